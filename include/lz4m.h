@@ -1,0 +1,146 @@
+/*
+ * include/lz4m.h -- C-ABI of the MI355X-native batched LZ4 block codec.
+ *
+ * Drop-in boundary for the python-lz4 hot path: the
+ * reference's CPython extensions (lz4/block/_block.c, lz4/frame/_frame.c)
+ * call into lz4libs/lz4.c and lz4libs/xxhash.c once per block; these entry
+ * points replace those calls with stream-ordered, batched HIP launches over
+ * device-resident blocks.  Plain pointers and sizes only: every pointer named
+ * d_* is a device (HBM) pointer, `stream` is a hipStream_t.  No entry point
+ * allocates, synchronises or touches host memory, so every call can be
+ * captured into a hipGraph.
+ *
+ * Return value of every launcher: 0 on success, otherwise a hipError_t value
+ * (launch failure) or LZ4M_EINVAL (bad argument).
+ *
+ * Per-block results follow the reference's own conventions:
+ *   - decompress status = decoded size, or -(input position)-1 at the point
+ *     where the input was rejected (lz4.c:2336-2337), bit-identical to
+ *     LZ4_decompress_safe / LZ4_decompress_safe_usingDict;
+ *   - compress length   = compressed size, or 0 when it does not fit in the
+ *     block's capacity (lz4.h:180-186, limitedOutput).
+ */
+#ifndef LZ4M_H
+#define LZ4M_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* lz4m_stream_t;   /* == hipStream_t */
+
+#define LZ4M_EINVAL 0x10000
+
+/* Match-finder table layouts:
+ *   U16_HASH4: LZ4_compress_default on blocks < 65547 B (lz4.c:1353-1354),
+ *              frame independent blocks (lz4.c:1399-1406);
+ *   U32_HASH5: lz4.block.compress (_block.c:109 -> LZ4_compress_fast_continue,
+ *              lz4.c:1671-1675) and LZ4_compress_default on >= 65547 B. */
+#define LZ4M_TABLE_U16_HASH4 0
+#define LZ4M_TABLE_U32_HASH5 1
+/* pick what LZ4_compress_default would pick for each block's size */
+#define LZ4M_TABLE_AUTO      2
+
+/* LZ4_compressBound (lz4.h:212 / lz4.c:730). */
+int lz4m_compress_bound(int input_size);
+
+/* Library identification (mirrors LZ4_versionNumber, lz4.c:728, of the
+ * format version this codec is bit-compatible with: 10904). */
+int lz4m_version_number(void);
+const char* lz4m_version_string(void);
+
+/*
+ * Batched LZ4_decompress_safe (lz4.h:191-205, lz4.c:2344-2350).
+ * Block i: input  d_src[d_src_off[i] .. + d_src_len[i]),
+ *          output d_dst[d_dst_off[i] .. + d_dst_cap[i]).
+ * d_status[i] = decoded size or -(pos)-1.  Bytes of a block's output slot
+ * beyond its decoded size are unspecified (as in the reference).  Output
+ * slots must not overlap.  Replaces the call at _block.c:357-359 and the
+ * per-block call in LZ4F_decompress (lz4frame.c:1844-1847).
+ */
+int lz4m_decompress_batch(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len,
+                          uint8_t* d_dst, const int64_t* d_dst_off, const int32_t* d_dst_cap,
+                          int32_t* d_status, int64_t n, lz4m_stream_t stream);
+
+/*
+ * Batched LZ4_decompress_safe_usingDict with the dictionary in a separate
+ * buffer (usingExtDict, lz4.c:2612-2625, the `dict=` argument of
+ * lz4.block.decompress, _block.c:357-359).  Dictionary i is
+ * d_dict[d_dict_off[i] .. + d_dict_len[i]); d_dict_len[i] == 0 means none.
+ */
+int lz4m_decompress_batch_dict(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len,
+                               uint8_t* d_dst, const int64_t* d_dst_off, const int32_t* d_dst_cap,
+                               const uint8_t* d_dict, const int64_t* d_dict_off, const int32_t* d_dict_len,
+                               int32_t* d_status, int64_t n, lz4m_stream_t stream);
+
+/*
+ * Batched greedy compressor, bit-exact with the reference parse for the
+ * chosen table layout (LZ4_compress_generic_validated, lz4.c:910-1302, fresh
+ * table per block).  acceleration as LZ4_compress_fast (clamped to
+ * [1, 65537], lz4.c:1350-1351).  d_out_len[i] = compressed size, or 0 when
+ * the block does not fit in d_dst_cap[i] bytes (limitedOutput).
+ * Replaces _block.c:233-235 (table U32_HASH5) and the per-block
+ * LZ4_compress_fast_extState_fastReset in LZ4F_compressBlock
+ * (lz4frame.c:853-863, table U16_HASH4 / AUTO).
+ */
+int lz4m_compress_batch(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len,
+                        uint8_t* d_dst, const int64_t* d_dst_off, const int32_t* d_dst_cap,
+                        int32_t* d_out_len, int64_t n, int table, int acceleration,
+                        lz4m_stream_t stream);
+
+/*
+ * Batched one-shot XXH32 (xxhash.c:392-416): d_out[i] = XXH32(block i, seed).
+ * Replaces the per-block checksum calls of lz4frame.c:846 (block checksum)
+ * and lz4frame.c:1819 (its verification).
+ */
+int lz4m_xxh32_batch(const uint8_t* d_src, const int64_t* d_off, const int64_t* d_len,
+                     uint32_t seed, uint32_t* d_out, int64_t n, lz4m_stream_t stream);
+
+/*
+ * XXH32 of one long buffer (the frame content checksum, lz4frame.c:1042 and
+ * :1171; XXH32_update/XXH32_digest over the whole content equal the one-shot
+ * XXH32 of it, total length mod 2^32, xxhash.c:464-554).  Serial by
+ * construction; runs on one wavefront.
+ */
+int lz4m_xxh32_long(const uint8_t* d_src, int64_t len, uint32_t seed, uint32_t* d_out,
+                    lz4m_stream_t stream);
+
+/*
+ * Exclusive prefix sum of n int32 sizes (+ per-item constant `add`) into
+ * int64 offsets starting at `base`; d_out has n+1 entries (the last one is
+ * the total).  d_scratch holds lz4m_scan_scratch_entries(n) int64 values.
+ * Used to compact variable-length block outputs.
+ */
+int64_t lz4m_scan_scratch_entries(int64_t n);
+int lz4m_exclusive_scan(const int32_t* d_len, int64_t add, int64_t base, int64_t* d_out,
+                        int64_t* d_scratch, int64_t n, lz4m_stream_t stream);
+
+/*
+ * Gather variable-length items into one contiguous buffer:
+ * d_out[d_out_off[i] .. + d_len[i]) = d_src[d_src_off[i] .. + d_len[i]).
+ */
+int lz4m_gather(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_len,
+                uint8_t* d_out, const int64_t* d_out_off, int64_t n, lz4m_stream_t stream);
+
+/*
+ * Frame block emission for independent blocks (LZ4F_makeBlock,
+ * lz4frame.c:825-850): for block i, with uncompressed bytes
+ * d_raw[d_raw_off[i] .. + d_raw_len[i]) and compressed bytes
+ * d_cmp[d_cmp_off[i] .. + d_cmp_len[i]) (0 = did not fit), writes at
+ * d_frame[d_frame_off[i]] the LE32 block size (bit 31 set for a stored raw
+ * block), the payload, and, if block_checksum, the LE32 XXH32 of the payload.
+ * d_frame_off comes from lz4m_frame_block_sizes + lz4m_exclusive_scan.
+ */
+int lz4m_frame_block_sizes(const int32_t* d_raw_len, const int32_t* d_cmp_len, int block_checksum,
+                           int32_t* d_rec_len, int64_t n, lz4m_stream_t stream);
+int lz4m_frame_emit(const uint8_t* d_raw, const int64_t* d_raw_off, const int32_t* d_raw_len,
+                    const uint8_t* d_cmp, const int64_t* d_cmp_off, const int32_t* d_cmp_len,
+                    uint8_t* d_frame, const int64_t* d_frame_off, int block_checksum,
+                    int64_t n, lz4m_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LZ4M_H */

@@ -1,0 +1,230 @@
+"""ctypes front-end for the CHECKERS (test infrastructure only).
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s
+``cpu_baseline`` leg import this module, and only to check or to time a
+baseline.  The shipped package (``python-lz4_amd/lz4``) never imports it.
+
+Two checkers live here:
+
+* ``Oracle`` -- the CPU restatement in ``oracle/lz4_oracle.c``
+  (``oracle/build/liboracle.so``);
+* ``Reference`` -- the reference ``lz4libs`` v1.9.4 compiled from
+  ``/root/reference`` by ``oracle/Makefile`` into ``oracle/_ref/``.  It is
+  used to pin the restatement and to generate ``tests/golden``; it is absent
+  on a box that never had the reference sources and no prebuilt ``_ref``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ORACLE_SO = os.path.join(HERE, "build", "liboracle.so")
+ORACLE_BENCH_SO = os.path.join(HERE, "build", "liboracle_bench.so")
+REF_SO = os.path.join(HERE, "_ref", "libref_lz4.so")
+REF_BENCH_SO = os.path.join(HERE, "_ref", "libref_bench.so")
+
+TABLE_U16_HASH4 = 0
+TABLE_U32_HASH5 = 1
+LIMIT_64K = 65536 + 11
+
+
+def build() -> None:
+    """Compile the checkers (restatement always; reference when present)."""
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def _buf(data) -> tuple:
+    arr = np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+    arr = np.ascontiguousarray(arr, dtype=np.uint8)
+    return arr, arr.ctypes.data_as(C.c_void_p)
+
+
+def compress_bound(n: int) -> int:
+    return 0 if n < 0 or n > 0x7E000000 else n + n // 255 + 16
+
+
+class Oracle:
+    """The CPU restatement."""
+
+    def __init__(self, path: str = ORACLE_SO):
+        if not os.path.exists(path):
+            build()
+        lib = C.CDLL(path)
+        vp, i32, i64, sz = C.c_void_p, C.c_int, C.c_int64, C.c_size_t
+        lib.orc_compress.argtypes = [vp, i32, vp, i32, i32, i32]
+        lib.orc_compress.restype = i32
+        lib.orc_decompress_dict.argtypes = [vp, vp, i32, i32, vp, sz]
+        lib.orc_decompress_dict.restype = i32
+        lib.orc_xxh32.argtypes = [vp, sz, C.c_uint32]
+        lib.orc_xxh32.restype = C.c_uint32
+        lib.orc_xxh32_state_size.restype = sz
+        lib.orc_xxh32_reset.argtypes = [vp, C.c_uint32]
+        lib.orc_xxh32_update.argtypes = [vp, vp, sz]
+        lib.orc_xxh32_digest.argtypes = [vp]
+        lib.orc_xxh32_digest.restype = C.c_uint32
+        lib.orc_compress_batch.argtypes = [vp, vp, vp, vp, vp, C.c_int32, vp, i64, i32, i32]
+        lib.orc_decompress_batch.argtypes = [vp, vp, vp, vp, vp, vp, vp, i64]
+        self.lib = lib
+
+    def compress(self, data, variant: int | None = None, accel: int = 1, cap: int | None = None) -> bytes | None:
+        """``variant`` None = LZ4_compress_default's choice by size."""
+        src, sp = _buf(data)
+        n = src.size
+        if variant is None:
+            variant = TABLE_U16_HASH4 if n < LIMIT_64K else TABLE_U32_HASH5
+        cap = compress_bound(n) if cap is None else cap
+        dst = np.zeros(max(cap, 1), dtype=np.uint8)
+        r = self.lib.orc_compress(sp, n, dst.ctypes.data_as(C.c_void_p), cap, variant, accel)
+        return None if r <= 0 else dst[:r].tobytes()
+
+    def decompress(self, data, cap: int, dict_=None) -> tuple[int, bytes]:
+        src, sp = _buf(data)
+        dst = np.zeros(max(cap, 1) + 64, dtype=np.uint8)
+        if dict_:
+            d, dp = _buf(dict_)
+            r = self.lib.orc_decompress_dict(sp, dst.ctypes.data_as(C.c_void_p), src.size, cap, dp, d.size)
+        else:
+            r = self.lib.orc_decompress_dict(sp, dst.ctypes.data_as(C.c_void_p), src.size, cap, None, 0)
+        return r, (dst[:r].tobytes() if r >= 0 else b"")
+
+    def xxh32(self, data, seed: int = 0) -> int:
+        src, sp = _buf(data)
+        return int(self.lib.orc_xxh32(sp, src.size, seed))
+
+    def xxh32_stream(self, chunks, seed: int = 0) -> int:
+        st = C.create_string_buffer(int(self.lib.orc_xxh32_state_size()))
+        self.lib.orc_xxh32_reset(st, seed)
+        for ch in chunks:
+            a, ap = _buf(ch)
+            self.lib.orc_xxh32_update(st, ap, a.size)
+        return int(self.lib.orc_xxh32_digest(st))
+
+
+class Reference:
+    """The reference lz4libs built from /root/reference by oracle/Makefile."""
+
+    def __init__(self, path: str = REF_SO):
+        if not os.path.exists(path):
+            build()
+        if not os.path.exists(path):
+            raise FileNotFoundError(path)
+        lib = C.CDLL(path)
+        vp, i32, sz = C.c_void_p, C.c_int, C.c_size_t
+        lib.LZ4_compress_default.argtypes = [vp, vp, i32, i32]
+        lib.LZ4_compress_default.restype = i32
+        lib.LZ4_compress_fast.argtypes = [vp, vp, i32, i32, i32]
+        lib.LZ4_compress_fast.restype = i32
+        lib.LZ4_decompress_safe.argtypes = [vp, vp, i32, i32]
+        lib.LZ4_decompress_safe.restype = i32
+        lib.LZ4_decompress_safe_usingDict.argtypes = [vp, vp, i32, i32, vp, i32]
+        lib.LZ4_decompress_safe_usingDict.restype = i32
+        lib.LZ4_sizeofState.restype = i32
+        lib.LZ4_resetStream.argtypes = [vp]
+        lib.LZ4_compress_fast_continue.argtypes = [vp, vp, vp, i32, i32, i32]
+        lib.LZ4_compress_fast_continue.restype = i32
+        lib.XXH32.argtypes = [vp, sz, C.c_uint32]
+        lib.XXH32.restype = C.c_uint32
+        lib.LZ4_versionNumber.restype = i32
+        lib.LZ4F_compressFrameBound.argtypes = [sz, vp]
+        lib.LZ4F_compressFrameBound.restype = sz
+        lib.LZ4F_compressFrame.argtypes = [vp, sz, vp, sz, vp]
+        lib.LZ4F_compressFrame.restype = sz
+        lib.LZ4F_isError.argtypes = [sz]
+        lib.LZ4F_isError.restype = C.c_uint
+        self.lib = lib
+
+    def version(self) -> int:
+        return int(self.lib.LZ4_versionNumber())
+
+    def compress_default(self, data) -> bytes:
+        src, sp = _buf(data)
+        cap = compress_bound(src.size)
+        dst = np.zeros(cap, dtype=np.uint8)
+        r = self.lib.LZ4_compress_default(sp, dst.ctypes.data_as(C.c_void_p), src.size, cap)
+        return dst[:r].tobytes()
+
+    def compress_block_api(self, data, accel: int = 1) -> bytes:
+        """lz4.block.compress(mode='default'|'fast', store_size=False): _block.c:93-121."""
+        src, sp = _buf(data)
+        cap = compress_bound(src.size)
+        dst = np.zeros(cap, dtype=np.uint8)
+        state = C.create_string_buffer(int(self.lib.LZ4_sizeofState()))
+        self.lib.LZ4_resetStream(state)
+        r = self.lib.LZ4_compress_fast_continue(state, sp, dst.ctypes.data_as(C.c_void_p), src.size, cap, accel)
+        return dst[:r].tobytes()
+
+    def decompress(self, data, cap: int, dict_=None) -> tuple[int, bytes]:
+        src, sp = _buf(data)
+        dst = np.zeros(max(cap, 1) + 64, dtype=np.uint8)
+        if dict_:
+            d, dp = _buf(dict_)
+            r = self.lib.LZ4_decompress_safe_usingDict(sp, dst.ctypes.data_as(C.c_void_p), src.size, cap, dp, d.size)
+        else:
+            r = self.lib.LZ4_decompress_safe(sp, dst.ctypes.data_as(C.c_void_p), src.size, cap)
+        return r, (dst[:r].tobytes() if r >= 0 else b"")
+
+    def xxh32(self, data, seed: int = 0) -> int:
+        src, sp = _buf(data)
+        return int(self.lib.XXH32(sp, src.size, seed))
+
+    def compress_frame(self, data, block_size_id: int = 7, linked: bool = False,
+                       content_checksum: bool = True, block_checksum: bool = False,
+                       store_size: bool = True, level: int = 0) -> bytes:
+        """LZ4F_compressFrame with explicit preferences (lz4frame.c:475-515)."""
+
+        class FrameInfo(C.Structure):
+            _fields_ = [("blockSizeID", C.c_int), ("blockMode", C.c_int),
+                        ("contentChecksumFlag", C.c_int), ("frameType", C.c_int),
+                        ("contentSize", C.c_ulonglong), ("dictID", C.c_uint),
+                        ("blockChecksumFlag", C.c_int)]
+
+        class Prefs(C.Structure):
+            _fields_ = [("frameInfo", FrameInfo), ("compressionLevel", C.c_int),
+                        ("autoFlush", C.c_uint), ("favorDecSpeed", C.c_uint),
+                        ("reserved", C.c_uint * 3)]
+
+        src, sp = _buf(data)
+        p = Prefs()
+        p.frameInfo.blockSizeID = block_size_id
+        p.frameInfo.blockMode = 0 if linked else 1
+        p.frameInfo.contentChecksumFlag = 1 if content_checksum else 0
+        p.frameInfo.blockChecksumFlag = 1 if block_checksum else 0
+        p.frameInfo.contentSize = src.size if store_size else 0
+        p.compressionLevel = level
+        cap = self.lib.LZ4F_compressFrameBound(src.size, C.byref(p))
+        dst = np.zeros(cap, dtype=np.uint8)
+        r = self.lib.LZ4F_compressFrame(dst.ctypes.data_as(C.c_void_p), cap, sp, src.size, C.byref(p))
+        if self.lib.LZ4F_isError(r):
+            raise RuntimeError("LZ4F_compressFrame failed")
+        return dst[:r].tobytes()
+
+
+class CpuBench:
+    """Throughput harness over the reference build (kind 'reference') or the
+    restatement (kind 'port')."""
+
+    def __init__(self):
+        if os.path.exists(REF_BENCH_SO):
+            self.kind, path = "reference", REF_BENCH_SO
+        else:
+            if not os.path.exists(ORACLE_BENCH_SO):
+                build()
+            self.kind, path = "port", ORACLE_BENCH_SO
+        lib = C.CDLL(path)
+        vp = C.c_void_p
+        lib.cpu_bench_run.argtypes = [C.c_int, C.c_int, C.c_int, vp, vp, vp, vp, vp, vp, vp, C.c_int64]
+        lib.cpu_bench_run.restype = C.c_double
+        self.lib = lib
+
+    def run(self, op: str, threads: int, reps: int, src: np.ndarray, src_off: np.ndarray,
+            src_len: np.ndarray, dst: np.ndarray, dst_off: np.ndarray, dst_cap: np.ndarray) -> tuple[float, np.ndarray]:
+        code = {"compress": 0, "decompress": 1, "xxh32": 2}[op]
+        out = np.zeros(src_off.size, dtype=np.int32)
+        ptr = lambda a: a.ctypes.data_as(C.c_void_p)
+        secs = self.lib.cpu_bench_run(code, threads, reps, ptr(src), ptr(src_off), ptr(src_len),
+                                      ptr(dst), ptr(dst_off), ptr(dst_cap), ptr(out), src_off.size)
+        return secs, out

@@ -1,0 +1,451 @@
+// lz4m_decompress.hip -- batched LZ4 block decoder for MI355X (gfx950).
+//
+// Bit-exact restatement of LZ4_decompress_safe / _usingDict (reference
+// lz4libs/lz4.c:1936-2339, x86_64 build with LZ4_FAST_DEC_LOOP=1): same
+// decoded bytes, same accept/reject decisions, same error position.
+//
+// Mapping.  One LANE owns one block and walks its sequences with the
+// reference's two-phase state machine (fast phase while >= 64 bytes of
+// output room, sticky switch to the safe phase).  A 64-lane wavefront thus
+// parses 64 blocks at once, so the serial token chain of each block costs one
+// lane, not one wave.  Short copies (the common case on compressible data:
+// literals <= 14 B, matches <= 18 B) are done by the owning lane with 16-byte
+// unaligned loads/stores.  Copies longer than kCoopMin are deferred: after
+// every sequence step the wave runs a cooperative phase in which all 64 lanes
+// execute each deferred copy at 1 KiB per wave instruction (coalesced), in
+// lane order, literal before match.  Incompressible blocks (one long literal
+// run) and run-length-heavy blocks therefore stream at wave width.
+//
+// Memory: compressed input is read once; the decoded output is written once
+// and match sources are re-read from the block's own output (L1/L2 hits, the
+// window is <= 64 KiB behind).  Algorithmic HBM bytes per block =
+// compressed size + decoded size.
+#include "lz4m_common.h"
+#include "../../include/lz4m.h"
+
+namespace lz4m {
+
+constexpr int64_t kCoopMin = 64;   // copies longer than this go wave-cooperative
+
+enum CopyKind : int { kNone = 0, kLiteral = 1, kMatch = 2 };
+
+struct Copy {
+    int kind;
+    int64_t dpos;    // destination position in the block's output
+    int64_t arg;     // literal: source position in the input; match: offset
+    int64_t len;
+};
+
+struct Lane {
+    const uint8_t* src;
+    uint8_t* dst;
+    const uint8_t* dict_end;
+    int64_t iend, oend, dict_len;
+    int64_t ip, op;
+    int32_t result;
+    bool fast, live;
+};
+
+// ---------------------------------------------------------------- lane copies
+// Non-overlapping copy by the owning lane.  Reads never pass s_room, writes
+// never pass d_room (the block's own buffers); inside those bounds the tail
+// may be copied as a full 16-byte chunk, like the reference's wild copies.
+__device__ __forceinline__ void lane_copy(uint8_t* d, const uint8_t* s, int64_t len, int64_t d_room,
+                                          int64_t s_room) {
+    for (int64_t i = 0; i < len; i += 16) {
+        if (len - i >= 16 || (d_room - i >= 16 && s_room - i >= 16)) {
+            st16(d + i, ld16(s + i));
+        } else {
+            for (int64_t k = i; k < len; ++k) d[k] = s[k];
+        }
+    }
+}
+
+// Overlapping LZ77 copy d[j] = d[j - off] (zeros when off == 0, lz4.c:478-485,
+// 2300-2307), by the owning lane.
+__device__ __forceinline__ void lane_match(uint8_t* d, int64_t off, int64_t len, int64_t room) {
+    if (off >= 16) {
+        for (int64_t i = 0; i < len; i += 16) {
+            if (len - i >= 16 || room - i >= 16) {
+                st16(d + i, ld16(d + i - off));
+            } else {
+                for (int64_t k = i; k < len; ++k) d[k] = d[k - off];
+            }
+        }
+        return;
+    }
+    u32x4 pat;
+    int64_t step;
+    if (off == 0) {
+        pat = u32x4{0, 0, 0, 0};
+        step = 16;
+    } else {
+        // the `off` bytes before d are final; read them (never past the slot)
+        const u32x4 w = ld16_guarded(d - off, off + (room < 16 - off ? room : 16 - off));
+        pat = period_pattern(w, (uint32_t)off);
+        step = 16 - (16 % off);
+    }
+    for (int64_t i = 0; i < len; i += step) {
+        if (room - i >= 16) {
+            st16(d + i, pat);
+        } else {
+            const int64_t e = len - i < 16 ? len - i : 16;
+            for (int k = 0; k < e; ++k) d[i + k] = (uint8_t)byte_of(pat, k);
+        }
+    }
+}
+
+// ---------------------------------------------------------- wave copies
+// All 64 lanes execute the same copy (uniform arguments).
+__device__ __forceinline__ void wave_literal(uint8_t* d, const uint8_t* s, int64_t len, int64_t d_room,
+                                             int64_t s_room, uint32_t lane) {
+    for (int64_t base = 0; base < len; base += 16 * kWave) {
+        const int64_t pos = base + 16 * (int64_t)lane;
+        if (pos < len) {
+            if (len - pos >= 16 || (d_room - pos >= 16 && s_room - pos >= 16)) {
+                st16(d + pos, ld16(s + pos));
+            } else {
+                for (int64_t k = pos; k < len; ++k) d[k] = s[k];
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ void wave_match(uint8_t* d, int64_t off, int64_t len, int64_t room, uint32_t lane) {
+    if (off >= 16) {
+        // rows of W bytes whose sources all lie before the row: W <= off
+        const int64_t w_bytes = ((off < 16 * kWave ? off : 16 * kWave) / 16) * 16;
+        for (int64_t base = 0; base < len; base += w_bytes) {
+            const int64_t pos = base + 16 * (int64_t)lane;
+            if (16 * (int64_t)lane < w_bytes && pos < len) {
+                if (len - pos >= 16 || room - pos >= 16) {
+                    st16(d + pos, ld16(d + pos - off));
+                } else {
+                    for (int64_t k = pos; k < len; ++k) d[k] = d[k - off];
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        }
+        return;
+    }
+    u32x4 pat;
+    int64_t step;
+    if (off == 0) {
+        pat = u32x4{0, 0, 0, 0};
+        step = 16;
+    } else {
+        const u32x4 w = ld16_guarded(d - off, off + (room < 16 - off ? room : 16 - off));
+        pat = period_pattern(w, (uint32_t)off);
+        step = 16 - (16 % off);
+    }
+    for (int64_t base = 0; base < len; base += step * kWave) {
+        const int64_t pos = base + step * (int64_t)lane;
+        if (pos < len) {
+            if (room - pos >= 16) {
+                st16(d + pos, pat);
+            } else {
+                const int64_t e = len - pos < 16 ? len - pos : 16;
+                for (int k = 0; k < e; ++k) d[pos + k] = (uint8_t)byte_of(pat, k);
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------ lane decode
+// read_variable_length (lz4.c:1903-1928).  On failure *ip is the position
+// the reference reports.
+__device__ __forceinline__ bool read_len(const uint8_t* src, int64_t& ip, int64_t ilimit, bool initial_check,
+                                         int64_t& out) {
+    if (initial_check && ip >= ilimit) return false;
+    int64_t len = 0;
+    uint32_t s;
+    do {
+        s = src[ip];
+        ++ip;
+        len += s;
+        if (ip > ilimit) return false;
+    } while (s == 255);
+    out = len;
+    return true;
+}
+
+__device__ __forceinline__ void emit_literal(Lane& L, int64_t ip, int64_t op, int64_t lit, Copy& c,
+                                             bool deferred) {
+    if (lit == 0) return;
+    if (deferred || lit > kCoopMin) {
+        c = Copy{kLiteral, op, ip, lit};
+    } else {
+        lane_copy(L.dst + op, L.src + ip, lit, L.oend - op, L.iend - ip);
+    }
+}
+
+__device__ __forceinline__ void emit_match(Lane& L, int64_t op, int64_t off, int64_t ml, Copy& c, bool deferred) {
+    if (deferred || ml > kCoopMin) {
+        c = Copy{kMatch, op, off, ml};
+    } else {
+        lane_match(L.dst + op, off, ml, L.oend - op);
+    }
+}
+
+// Match that starts inside the external dictionary (lz4.c:2252-2277).
+// Rare; done by the owning lane.
+__device__ __noinline__ void dict_match(Lane& L, int64_t op, int64_t off, int64_t ml) {
+    const int64_t in_dict = off - op;
+    uint8_t* d = L.dst + op;
+    const uint8_t* s = L.dict_end - in_dict;
+    if (ml <= in_dict) {
+        for (int64_t k = 0; k < ml; ++k) d[k] = s[k];
+    } else {
+        for (int64_t k = 0; k < in_dict; ++k) d[k] = s[k];
+        const int64_t rest = ml - in_dict;
+        uint8_t* d2 = d + in_dict;
+        const int64_t off2 = op + in_dict;   // continues from the block start
+        for (int64_t k = 0; k < rest; ++k) d2[k] = d2[k - off2];
+    }
+}
+
+// One sequence of block L.  Deferred copies land in lc / mc.
+template <bool DICT>
+__device__ void decode_step(Lane& L, Copy& lc, Copy& mc) {
+    const u32x4 w = ld16_guarded(L.src + L.ip, L.iend - L.ip);
+    const uint32_t tok = w.x & 0xFFu;
+    int64_t ip = L.ip + 1;
+    int64_t op = L.op;
+    int64_t lit = tok >> 4, ml, off, add;
+    bool deferred = false;
+    const int64_t iend = L.iend, oend = L.oend;
+    const int64_t dlen = DICT ? L.dict_len : 0;
+    const bool check_window = dlen < 65536;
+#define OOW(o) (check_window && (o) > op + dlen)
+
+    if (L.fast) {   // lz4.c:1996-2109
+        if (lit == 15) {
+            if (!read_len(L.src, ip, iend - 15, true, add)) goto fail;
+            lit += add;
+            if (op + lit > oend - 32 || ip + lit > iend - 32) {
+                L.fast = false;
+                goto literal_tail;
+            }
+            emit_literal(L, ip, op, lit, lc, false);
+            deferred = lc.kind != kNone;
+            ip += lit;
+            op += lit;
+            off = ld16le(L.src + ip);
+        } else {
+            if (ip > iend - 17) {
+                L.fast = false;
+                goto literal_tail;
+            }
+            // literals are bytes 1..lit of the token window (wild 16-byte store)
+            st16(L.dst + op, window_shift1(w));
+            off = lit <= 13 ? (window_dword(w, (uint32_t)(1 + lit)) & 0xFFFFu) : ld16le(L.src + ip + lit);
+            ip += lit;
+            op += lit;
+        }
+        ip += 2;
+        ml = tok & 15;
+        if (ml == 15) {
+            if (!read_len(L.src, ip, iend - 4, false, add)) goto fail;
+            ml += add + 4;
+            if (OOW(off)) goto fail;
+            if (op + ml >= oend - 64) {
+                L.fast = false;
+                goto match_tail;
+            }
+        } else {
+            ml += 4;
+            if (op + ml >= oend - 64) {
+                L.fast = false;
+                goto match_tail;
+            }
+            if (off >= 8 && off <= op) {
+                emit_match(L, op, off, ml, mc, deferred);
+                op += ml;
+                goto done;
+            }
+        }
+        if (OOW(off)) goto fail;
+        if (DICT && off > op) {
+            if (op + ml > oend - 5) goto fail;
+            if (deferred) goto defer_dict;
+            dict_match(L, op, off, ml);
+            op += ml;
+            goto done;
+        }
+        emit_match(L, op, off, ml, mc, deferred);
+        op += ml;
+        goto done;
+    }
+
+    // safe phase, lz4.c:2114-2329
+    if (lit != 15 && ip < iend - 16 && op <= oend - 32) {   // shortcut, lz4.c:2128-2158
+        st16(L.dst + op, window_shift1(w));
+        off = lit <= 13 ? (window_dword(w, (uint32_t)(1 + lit)) & 0xFFFFu) : ld16le(L.src + ip + lit);
+        op += lit;
+        ip += lit + 2;
+        ml = tok & 15;
+        if (ml != 15 && off >= 8 && off <= op) {
+            lane_match(L.dst + op, off, ml + 4, oend - op);
+            op += ml + 4;
+            goto done;
+        }
+        goto match_length;
+    }
+    if (lit == 15) {
+        if (!read_len(L.src, ip, iend - 15, true, add)) goto fail;
+        lit += add;
+    }
+literal_tail:   // lz4.c:2172-2229
+    if (op + lit > oend - 12 || ip + lit > iend - 8) {
+        if (ip + lit != iend || op + lit > oend) goto fail;
+        emit_literal(L, ip, op, lit, lc, false);   // last literals: exact (never past oend / iend)
+        op += lit;
+        L.result = (int32_t)op;
+        L.live = false;
+        L.op = op;
+        return;
+    }
+    emit_literal(L, ip, op, lit, lc, false);
+    deferred = lc.kind != kNone;
+    ip += lit;
+    op += lit;
+    off = ld16le(L.src + ip);
+    ip += 2;
+    ml = tok & 15;
+match_length:   // lz4.c:2238-2245
+    if (ml == 15) {
+        if (!read_len(L.src, ip, iend - 4, false, add)) goto fail;
+        ml += add;
+    }
+    ml += 4;
+match_tail:   // lz4.c:2248-2328
+    if (OOW(off)) goto fail;
+    if (DICT && off > op) {
+        if (op + ml > oend - 5) goto fail;
+        if (deferred) goto defer_dict;
+        dict_match(L, op, off, ml);
+        op += ml;
+        goto done;
+    }
+    if (op + ml > oend - 5) goto fail;
+    emit_match(L, op, off, ml, mc, deferred);
+    op += ml;
+done:
+    L.ip = ip;
+    L.op = op;
+    return;
+defer_dict:
+    // a dictionary match behind a deferred literal: run it right after the
+    // cooperative phase by re-entering with a pending marker
+    mc = Copy{kMatch, op, -off, ml};   // negative offset marks "dictionary"
+    op += ml;
+    goto done;
+fail:
+    L.result = (int32_t)(-ip - 1);
+    L.live = false;
+    return;
+#undef OOW
+}
+
+template <bool DICT>
+__global__ __launch_bounds__(256) void decompress_kernel(const uint8_t* __restrict__ src,
+                                                         const int64_t* __restrict__ src_off,
+                                                         const int32_t* __restrict__ src_len, uint8_t* dst,
+                                                         const int64_t* __restrict__ dst_off,
+                                                         const int32_t* __restrict__ dst_cap,
+                                                         const uint8_t* __restrict__ dict,
+                                                         const int64_t* __restrict__ dict_off,
+                                                         const int32_t* __restrict__ dict_len,
+                                                         int32_t* __restrict__ status, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t lane = lane_id();
+    Lane L;
+    L.live = false;
+    L.result = -1;
+    if (i < n) {
+        L.src = src + src_off[i];
+        L.dst = dst + dst_off[i];
+        L.iend = src_len[i];
+        L.oend = dst_cap[i];
+        L.ip = 0;
+        L.op = 0;
+        L.dict_len = 0;
+        L.dict_end = nullptr;
+        if (DICT) {
+            L.dict_len = dict_len[i];
+            L.dict_end = dict + dict_off[i] + L.dict_len;
+        }
+        if (L.oend < 0) {
+            L.result = -1;   // lz4.c:1950
+        } else if (L.oend == 0) {
+            L.result = (L.iend == 1 && L.src[0] == 0) ? 0 : -1;   // lz4.c:1978-1982
+        } else if (L.iend <= 0) {
+            L.result = -1;   // lz4.c:1983
+        } else {
+            L.fast = L.oend >= 64;
+            L.live = true;
+        }
+    }
+
+    while (__any(L.live)) {
+        Copy lc{kNone, 0, 0, 0}, mc{kNone, 0, 0, 0};
+        if (L.live) decode_step<DICT>(L, lc, mc);
+        uint64_t pend = __ballot(lc.kind != kNone || mc.kind != kNone);
+        if (pend == 0) continue;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // lane stores visible to the wave
+        while (pend) {
+            const int l = __builtin_ctzll(pend);
+            pend &= pend - 1;
+            uint8_t* d = readlane_ptr(L.dst, l);
+            const int64_t oend = readlane64(L.oend, l);
+            const int lk = __builtin_amdgcn_readlane(lc.kind, l);
+            if (lk != kNone) {
+                const uint8_t* s = readlane_ptr(L.src, l);
+                const int64_t iend = readlane64(L.iend, l);
+                const int64_t dp = readlane64(lc.dpos, l), sp = readlane64(lc.arg, l), ln = readlane64(lc.len, l);
+                wave_literal(d + dp, s + sp, ln, oend - dp, iend - sp, lane);
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            }
+            const int mk = __builtin_amdgcn_readlane(mc.kind, l);
+            if (mk != kNone) {
+                const int64_t dp = readlane64(mc.dpos, l), off = readlane64(mc.arg, l), ln = readlane64(mc.len, l);
+                if (DICT && off < 0) {
+                    if (lane == (uint32_t)l) dict_match(L, dp, -off, ln);
+                } else {
+                    wave_match(d + dp, off, ln, oend - dp, lane);
+                }
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            }
+        }
+    }
+    if (i < n) status[i] = L.result;
+}
+
+}  // namespace lz4m
+
+using namespace lz4m;
+
+extern "C" int lz4m_decompress_batch(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len,
+                                     uint8_t* d_dst, const int64_t* d_dst_off, const int32_t* d_dst_cap,
+                                     int32_t* d_status, int64_t n, lz4m_stream_t stream) {
+    if (n < 0) return LZ4M_EINVAL;
+    if (n == 0) return 0;
+    const int64_t grid = (n + 255) / 256;
+    hipLaunchKernelGGL(decompress_kernel<false>, dim3((uint32_t)grid), dim3(256), 0, (hipStream_t)stream, d_src,
+                       d_src_off, d_src_len, d_dst, d_dst_off, d_dst_cap, nullptr, nullptr, nullptr, d_status, n);
+    return (int)hipGetLastError();
+}
+
+extern "C" int lz4m_decompress_batch_dict(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len,
+                                          uint8_t* d_dst, const int64_t* d_dst_off, const int32_t* d_dst_cap,
+                                          const uint8_t* d_dict, const int64_t* d_dict_off,
+                                          const int32_t* d_dict_len, int32_t* d_status, int64_t n,
+                                          lz4m_stream_t stream) {
+    if (n < 0) return LZ4M_EINVAL;
+    if (n == 0) return 0;
+    const int64_t grid = (n + 255) / 256;
+    hipLaunchKernelGGL(decompress_kernel<true>, dim3((uint32_t)grid), dim3(256), 0, (hipStream_t)stream, d_src,
+                       d_src_off, d_src_len, d_dst, d_dst_off, d_dst_cap, d_dict, d_dict_off, d_dict_len, d_status,
+                       n);
+    return (int)hipGetLastError();
+}

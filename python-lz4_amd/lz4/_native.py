@@ -1,0 +1,172 @@
+"""Binding to the HIP C-ABI library ``_lz4m.so`` (include/lz4m.h).
+
+The library is loaded into the process's HIP runtime -- the one PyTorch-ROCm
+already loaded (same SONAME, libamdhip64.so.7) -- so device pointers of torch
+tensors and torch's current HIP stream are passed straight through.
+
+There is no CPU code path behind this module: if the library or a HIP device
+is missing, every entry point raises ``RuntimeError``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lz4m.so")
+
+TABLE_U16_HASH4 = 0
+TABLE_U32_HASH5 = 1
+TABLE_AUTO = 2
+EINVAL = 0x10000
+
+_lock = threading.Lock()
+_lib = None
+
+
+def _declare(lib) -> None:
+    vp, i32, i64, u32 = C.c_void_p, C.c_int, C.c_int64, C.c_uint32
+    sig = {
+        "lz4m_compress_bound": ([i32], i32),
+        "lz4m_version_number": ([], i32),
+        "lz4m_version_string": ([], C.c_char_p),
+        "lz4m_decompress_batch": ([vp, vp, vp, vp, vp, vp, vp, i64, vp], i32),
+        "lz4m_decompress_batch_dict": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, vp], i32),
+        "lz4m_compress_batch": ([vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, vp], i32),
+        "lz4m_xxh32_batch": ([vp, vp, vp, u32, vp, i64, vp], i32),
+        "lz4m_xxh32_long": ([vp, i64, u32, vp, vp], i32),
+        "lz4m_scan_scratch_entries": ([i64], i64),
+        "lz4m_exclusive_scan": ([vp, i64, i64, vp, vp, i64, vp], i32),
+        "lz4m_gather": ([vp, vp, vp, vp, vp, i64, vp], i32),
+        "lz4m_frame_block_sizes": ([vp, vp, i32, vp, i64, vp], i32),
+        "lz4m_frame_emit": ([vp, vp, vp, vp, vp, vp, vp, vp, i32, i64, vp], i32),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+
+
+def lib():
+    """The loaded C-ABI library (raises if it is missing)."""
+    global _lib
+    if _lib is None:
+        with _lock:
+            if _lib is None:
+                if not os.path.exists(LIB_PATH):
+                    raise RuntimeError(
+                        f"lz4 MI355X backend not built: {LIB_PATH} is missing "
+                        "(run `make -C python-lz4_amd/csrc` or __graft_entry__.build())")
+                l = C.CDLL(LIB_PATH)
+                _declare(l)
+                _lib = l
+    return _lib
+
+
+def device() -> torch.device:
+    if not torch.cuda.is_available():
+        raise RuntimeError("lz4 MI355X backend: no HIP device is visible; this package has no CPU code path")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def stream_ptr(stream=None) -> int:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return int(s.cuda_stream)
+
+
+def ptr(t: torch.Tensor | None) -> int | None:
+    return None if t is None else int(t.data_ptr())
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise RuntimeError(f"{what} failed to launch (code {rc:#x})")
+
+
+def compress_bound(n: int) -> int:
+    """LZ4_compressBound (lz4.h:212)."""
+    return 0 if n < 0 or n > 0x7E000000 else n + n // 255 + 16
+
+
+# ------------------------------------------------------------ raw launchers
+def launch_decompress(src, src_off, src_len, dst, dst_off, dst_cap, status, n, stream=None,
+                      dict_buf=None, dict_off=None, dict_len=None) -> None:
+    L = lib()
+    sp = stream_ptr(stream)
+    if dict_buf is None:
+        rc = L.lz4m_decompress_batch(ptr(src), ptr(src_off), ptr(src_len), ptr(dst), ptr(dst_off), ptr(dst_cap),
+                                     ptr(status), n, sp)
+    else:
+        rc = L.lz4m_decompress_batch_dict(ptr(src), ptr(src_off), ptr(src_len), ptr(dst), ptr(dst_off),
+                                          ptr(dst_cap), ptr(dict_buf), ptr(dict_off), ptr(dict_len), ptr(status),
+                                          n, sp)
+    check(rc, "lz4m_decompress_batch")
+
+
+def launch_compress(src, src_off, src_len, dst, dst_off, dst_cap, out_len, n, table, accel, stream=None) -> None:
+    rc = lib().lz4m_compress_batch(ptr(src), ptr(src_off), ptr(src_len), ptr(dst), ptr(dst_off), ptr(dst_cap),
+                                   ptr(out_len), n, table, accel, stream_ptr(stream))
+    check(rc, "lz4m_compress_batch")
+
+
+def launch_xxh32_batch(src, off, length, seed, out, n, stream=None) -> None:
+    rc = lib().lz4m_xxh32_batch(ptr(src), ptr(off), ptr(length), seed & 0xFFFFFFFF, ptr(out), n, stream_ptr(stream))
+    check(rc, "lz4m_xxh32_batch")
+
+
+def launch_xxh32_long(src, length, seed, out, stream=None) -> None:
+    rc = lib().lz4m_xxh32_long(ptr(src), length, seed & 0xFFFFFFFF, ptr(out), stream_ptr(stream))
+    check(rc, "lz4m_xxh32_long")
+
+
+def exclusive_scan(lengths: torch.Tensor, add: int = 0, base: int = 0, stream=None) -> torch.Tensor:
+    """int64 offsets (n+1 entries, last = total) of int32 ``lengths`` (+add each)."""
+    n = lengths.numel()
+    out = torch.empty(n + 1, dtype=torch.int64, device=lengths.device)
+    scratch = torch.empty(int(lib().lz4m_scan_scratch_entries(n)), dtype=torch.int64, device=lengths.device)
+    rc = lib().lz4m_exclusive_scan(ptr(lengths), add, base, ptr(out), ptr(scratch), n, stream_ptr(stream))
+    check(rc, "lz4m_exclusive_scan")
+    return out
+
+
+def gather(src, src_off, length, out, out_off, n, stream=None) -> None:
+    rc = lib().lz4m_gather(ptr(src), ptr(src_off), ptr(length), ptr(out), ptr(out_off), n, stream_ptr(stream))
+    check(rc, "lz4m_gather")
+
+
+def frame_block_sizes(raw_len, cmp_len, block_checksum, rec_len, n, stream=None) -> None:
+    rc = lib().lz4m_frame_block_sizes(ptr(raw_len), ptr(cmp_len), int(bool(block_checksum)), ptr(rec_len), n,
+                                      stream_ptr(stream))
+    check(rc, "lz4m_frame_block_sizes")
+
+
+def frame_emit(raw, raw_off, raw_len, cmp, cmp_off, cmp_len, frame, frame_off, block_checksum, n,
+               stream=None) -> None:
+    rc = lib().lz4m_frame_emit(ptr(raw), ptr(raw_off), ptr(raw_len), ptr(cmp), ptr(cmp_off), ptr(cmp_len),
+                               ptr(frame), ptr(frame_off), int(bool(block_checksum)), n, stream_ptr(stream))
+    check(rc, "lz4m_frame_emit")
+
+
+# ------------------------------------------------------------ host <-> device
+def to_device(buf, dev=None, pad: int = 0) -> torch.Tensor:
+    """Copy a bytes-like object to a device uint8 tensor (+pad zero bytes)."""
+    dev = dev or device()
+    mv = memoryview(buf).cast("B")
+    n = mv.nbytes
+    out = torch.empty(n + pad, dtype=torch.uint8, device=dev)
+    if n:
+        host = torch.frombuffer(bytearray(mv) if mv.readonly else mv, dtype=torch.uint8)
+        out[:n].copy_(host, non_blocking=False)
+    if pad:
+        out[n:].zero_()
+    return out
+
+
+def to_host_bytes(t: torch.Tensor, n: int, as_bytearray: bool = False):
+    if n == 0:
+        return bytearray() if as_bytearray else b""
+    h = t[:n].cpu().numpy()
+    return bytearray(h.tobytes()) if as_bytearray else h.tobytes()

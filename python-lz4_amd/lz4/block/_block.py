@@ -1,0 +1,330 @@
+"""``lz4.block`` on the MI355X codec.
+
+Drop-in for the reference CPython extension ``lz4/block/_block.c``: same
+function names, argument handling, return types, size header and exception
+messages (``_block.c:127-400``).  Every call runs the HIP kernels of
+``_lz4m.so``; single calls pay one H2D + launch + D2H, so the batched
+entry points (``compress_batch`` / ``decompress_batch`` on device tensors,
+``compress_many`` / ``decompress_many`` on host buffers) are the throughput
+path.
+"""
+from __future__ import annotations
+
+import operator
+
+import torch
+
+from .. import _native as N
+
+INT_MAX = 2**31 - 1
+INT_MIN = -(2**31)
+_HDR = 4   # _block.c:82, LE32 uncompressed size prefix
+
+# lz4hc.h:47-50, exported by _block.c:508-511
+HC_LEVEL_MIN = 3
+HC_LEVEL_DEFAULT = 9
+HC_LEVEL_OPT_MIN = 10
+HC_LEVEL_MAX = 12
+
+
+class LZ4BlockError(Exception):
+    """Call to LZ4 library failed."""
+
+
+LZ4BlockError.__module__ = "_block"
+
+
+# -------------------------------------------------------------- arg helpers
+def _c_int(value, name: str) -> int:
+    """PyArg 'i' conversion: __index__ required, C int range enforced."""
+    try:
+        v = operator.index(value)
+    except TypeError:
+        raise TypeError(f"'{type(value).__name__}' object cannot be interpreted as an integer") from None
+    if v > INT_MAX:
+        raise OverflowError("signed integer is greater than maximum")
+    if v < INT_MIN:
+        raise OverflowError("signed integer is less than minimum")
+    return v
+
+
+def _buffer(obj, name: str = "source") -> memoryview:
+    """PyArg 'y*' conversion: any contiguous buffer; str is rejected."""
+    if isinstance(obj, str):
+        raise TypeError(f"a bytes-like object is required, not '{type(obj).__name__}'")
+    mv = memoryview(obj)
+    if not mv.c_contiguous:
+        raise BufferError("memoryview: underlying buffer is not C-contiguous")
+    return mv.cast("B") if mv.format != "B" or mv.ndim != 1 else mv
+
+
+def _mode_accel(mode, acceleration: int) -> int:
+    if not isinstance(mode, str):
+        raise TypeError(f"compress() argument 'mode' must be str, not {type(mode).__name__}")
+    if mode == "default":
+        return 1
+    if mode == "fast":
+        return acceleration
+    if mode == "high_compression":
+        raise NotImplementedError(
+            "mode='high_compression' (LZ4 HC) is outside the MI355X codec's scope; "
+            "use mode='default' or mode='fast'")
+    raise ValueError(f"Invalid mode argument: {mode}. Must be one of: standard, fast, high_compression")
+
+
+def _i64(vals, dev) -> torch.Tensor:
+    return torch.tensor(vals, dtype=torch.int64, device=dev)
+
+
+def _i32(vals, dev) -> torch.Tensor:
+    return torch.tensor(vals, dtype=torch.int32, device=dev)
+
+
+# ------------------------------------------------------------ single calls
+def compress(source, mode="default", store_size=True, acceleration=1, compression=9,
+             return_bytearray=False, dict=None):
+    """compress(source, mode='default', acceleration=1, compression=0, return_bytearray=False)
+
+    Compress source into one LZ4 block (``_block.c:127-271``), output
+    byte-identical to the reference: ``lz4.block.compress`` resets an
+    ``LZ4_stream_t`` and calls ``LZ4_compress_fast_continue`` (byU32 table,
+    hash5), which ``TABLE_U32_HASH5`` reproduces.
+    """
+    src = _buffer(source)
+    acceleration = _c_int(acceleration, "acceleration")
+    _c_int(compression, "compression")
+    if src.nbytes > INT_MAX:
+        raise OverflowError("Input too large for LZ4 API")
+    if dict is not None:
+        d = _buffer(dict, "dict")
+        if d.nbytes > INT_MAX:
+            raise OverflowError("Dictionary too large for LZ4 API")
+        if d.nbytes:
+            raise NotImplementedError("compress(dict=...) is not provided by the MI355X codec yet")
+    accel = _mode_accel(mode, acceleration)
+    out = compress_many([src], accel=accel, store_size=bool(store_size), as_bytearray=bool(return_bytearray))[0]
+    if out is None:
+        raise LZ4BlockError("Compression failed")
+    return out
+
+
+def decompress(source, uncompressed_size=-1, return_bytearray=False, dict=None):
+    """decompress(source, uncompressed_size=-1, return_bytearray=False)
+
+    Decompress one LZ4 block (``_block.c:273-400``).  With
+    ``uncompressed_size >= 0`` the whole source is the block and the value is
+    a capacity; otherwise a LE32 size header leads the block and the decoded
+    size must equal it.
+    """
+    src = _buffer(source)
+    uncompressed_size = _c_int(uncompressed_size, "uncompressed_size")
+    if src.nbytes > INT_MAX:
+        raise OverflowError("Input too large for LZ4 API")
+    dview = None
+    if dict is not None:
+        dview = _buffer(dict, "dict")
+        if dview.nbytes > INT_MAX:
+            raise OverflowError("Dictionary too large for LZ4 API")
+    res = decompress_many([src], uncompressed_size=uncompressed_size, dict=dview,
+                          as_bytearray=bool(return_bytearray), raise_errors=True)
+    return res[0]
+
+
+# ---------------------------------------------------- host-buffer batches
+def _pack_host(views) -> tuple[bytearray, list[int], list[int]]:
+    offs, lens, total = [], [], 0
+    for v in views:
+        offs.append(total)
+        lens.append(v.nbytes)
+        total += v.nbytes
+    packed = bytearray(total)
+    for v, o in zip(views, offs):
+        packed[o:o + v.nbytes] = v
+    return packed, offs, lens
+
+
+def compress_many(blocks, accel: int = 1, store_size: bool = True, as_bytearray: bool = False,
+                  table: int = N.TABLE_U32_HASH5):
+    """Compress a sequence of host buffers as independent blocks in one
+    launch.  Returns a list of bytes (None for a block that failed, i.e.
+    input larger than LZ4_MAX_INPUT_SIZE)."""
+    views = [_buffer(b) for b in blocks]
+    dev = N.device()
+    packed, offs, lens = _pack_host(views)
+    n = len(views)
+    caps = [max(N.compress_bound(L), 1) for L in lens]
+    d_off = [0] * n
+    acc = 0
+    for i, c in enumerate(caps):
+        d_off[i] = acc
+        acc += c
+    d_src = N.to_device(packed, dev)
+    d_dst = torch.empty(max(acc, 1), dtype=torch.uint8, device=dev)
+    src_off, src_len = _i64(offs, dev), _i32(lens, dev)
+    dst_off, dst_cap = _i64(d_off, dev), _i32(caps, dev)
+    out_len = torch.empty(n, dtype=torch.int32, device=dev)
+    N.launch_compress(d_src, src_off, src_len, d_dst, dst_off, dst_cap, out_len, n, table, accel)
+    host = d_dst.cpu().numpy()
+    olen = out_len.cpu().tolist()
+    res = []
+    for i in range(n):
+        L = olen[i]
+        if L <= 0:
+            res.append(None)
+            continue
+        body = host[d_off[i]:d_off[i] + L].tobytes()
+        if store_size:
+            body = lens[i].to_bytes(4, "little") + body
+        res.append(bytearray(body) if as_bytearray else body)
+    return res
+
+
+def decompress_many(blocks, uncompressed_size=-1, dict=None, as_bytearray: bool = False,
+                    raise_errors: bool = True):
+    """Decompress a sequence of host buffers in one launch.
+
+    ``uncompressed_size`` is one int for all blocks or a list; negative
+    means "read the LE32 size header".  With ``raise_errors`` the first
+    failing block raises the reference's exception; otherwise failing blocks
+    yield the LZ4BlockError instance in their slot.
+    """
+    views = [_buffer(b) for b in blocks]
+    n = len(views)
+    sizes = list(uncompressed_size) if isinstance(uncompressed_size, (list, tuple)) else [uncompressed_size] * n
+    caps, skip, errors = [], [], [None] * n
+    for i, (v, us) in enumerate(zip(views, sizes)):
+        if us >= 0:
+            caps.append(us)
+            skip.append(0)
+        else:
+            if v.nbytes < _HDR:
+                err = ValueError("Input source data size too small")
+                if raise_errors:
+                    raise err
+                errors[i] = err
+                caps.append(0)
+                skip.append(0)
+                continue
+            cap = int.from_bytes(v[:4], "little")
+            if cap > INT_MAX:
+                err = ValueError(f"Invalid size: 0x{cap}")
+                if raise_errors:
+                    raise err
+                errors[i] = err
+                caps.append(0)
+                skip.append(0)
+                continue
+            caps.append(cap)
+            skip.append(_HDR)
+    dev = N.device()
+    packed, offs, lens = _pack_host(views)
+    d_src = N.to_device(packed, dev)
+    src_off = _i64([o + s for o, s in zip(offs, skip)], dev)
+    src_len = _i32([L - s for L, s in zip(lens, skip)], dev)
+    d_off, acc = [], 0
+    for c in caps:
+        d_off.append(acc)
+        acc += c
+    d_dst = torch.empty(max(acc, 1), dtype=torch.uint8, device=dev)
+    dst_off, dst_cap = _i64(d_off, dev), _i32(caps, dev)
+    status = torch.empty(n, dtype=torch.int32, device=dev)
+    if dict is not None and _buffer(dict).nbytes:
+        dv = _buffer(dict)
+        d_dict = N.to_device(dv, dev)
+        N.launch_decompress(d_src, src_off, src_len, d_dst, dst_off, dst_cap, status, n,
+                            dict_buf=d_dict, dict_off=torch.zeros(n, dtype=torch.int64, device=dev),
+                            dict_len=torch.full((n,), dv.nbytes, dtype=torch.int32, device=dev))
+    else:
+        N.launch_decompress(d_src, src_off, src_len, d_dst, dst_off, dst_cap, status, n)
+    st = status.cpu().tolist()
+    host = d_dst.cpu().numpy() if acc else None
+    res = []
+    for i in range(n):
+        if errors[i] is not None:
+            res.append(errors[i])
+            continue
+        r = st[i]
+        err = None
+        if r < 0:
+            err = LZ4BlockError(
+                "Decompression failed: corrupt input or insufficient space in destination buffer. "
+                f"Error code: {-r}")
+        elif r != caps[i] and sizes[i] < 0:
+            err = LZ4BlockError(f"Decompressor wrote {r} bytes, but {caps[i]} bytes expected from header")
+        if err is not None:
+            if raise_errors:
+                raise err
+            res.append(err)
+            continue
+        body = host[d_off[i]:d_off[i] + r].tobytes() if r else b""
+        res.append(bytearray(body) if as_bytearray else body)
+    return res
+
+
+# ------------------------------------------------- device-resident batches
+def compress_batch(src: torch.Tensor, src_off: torch.Tensor, src_len: torch.Tensor, *,
+                   table: str | int = "block", acceleration: int = 1, dst: torch.Tensor | None = None,
+                   dst_off: torch.Tensor | None = None, dst_cap: torch.Tensor | None = None, stream=None):
+    """Compress n device-resident blocks in one stream-ordered launch.
+
+    ``src`` uint8 (HBM), ``src_off`` int64[n], ``src_len`` int32[n].
+    ``table``: "block" (lz4.block.compress parse, byU32/hash5), "default"
+    (LZ4_compress_default's choice by size; byU16/hash4 below 65547 B) or a
+    TABLE_* constant.  Output slots default to LZ4_compressBound(len) each.
+    Returns (dst, dst_off, out_len) with out_len int32[n] (0 = did not fit).
+    No host synchronisation.
+    """
+    tab = {"block": N.TABLE_U32_HASH5, "default": N.TABLE_AUTO, "u16": N.TABLE_U16_HASH4}.get(table, table)
+    n = src_off.numel()
+    dev = src.device
+    if dst_cap is None:
+        dst_cap = (src_len.to(torch.int64) + src_len.to(torch.int64) // 255 + 16).to(torch.int32)
+    if dst_off is None:
+        dst_off = N.exclusive_scan(dst_cap, stream=stream)[:n]
+    if dst is None:
+        total = int((dst_off[-1] + dst_cap[-1]).item()) if n else 1
+        dst = torch.empty(max(total, 1), dtype=torch.uint8, device=dev)
+    out_len = torch.empty(n, dtype=torch.int32, device=dev)
+    N.launch_compress(src, src_off, src_len, dst, dst_off, dst_cap, out_len, n, int(tab), int(acceleration), stream)
+    return dst, dst_off, out_len
+
+
+def decompress_batch(src: torch.Tensor, src_off: torch.Tensor, src_len: torch.Tensor, dst_cap: torch.Tensor, *,
+                     dst: torch.Tensor | None = None, dst_off: torch.Tensor | None = None,
+                     dict_buf: torch.Tensor | None = None, dict_off: torch.Tensor | None = None,
+                     dict_len: torch.Tensor | None = None, stream=None):
+    """Decompress n device-resident blocks in one stream-ordered launch.
+
+    Returns (dst, dst_off, status): status int32[n] is the decoded size or
+    -(pos)-1 exactly as LZ4_decompress_safe(_usingDict) would return.
+    """
+    n = src_off.numel()
+    dev = src.device
+    if dst_off is None:
+        dst_off = N.exclusive_scan(dst_cap, stream=stream)[:n]
+    if dst is None:
+        total = int((dst_off[-1] + dst_cap[-1]).item()) if n else 1
+        dst = torch.empty(max(total, 1), dtype=torch.uint8, device=dev)
+    status = torch.empty(n, dtype=torch.int32, device=dev)
+    N.launch_decompress(src, src_off, src_len, dst, dst_off, dst_cap, status, n, stream,
+                        dict_buf, dict_off, dict_len)
+    return dst, dst_off, status
+
+
+def compact(buf: torch.Tensor, off: torch.Tensor, length: torch.Tensor, stream=None):
+    """Pack variable-length items (e.g. compress_batch output) contiguously:
+    returns (packed uint8, offsets int64[n+1])."""
+    n = off.numel()
+    offs = N.exclusive_scan(length, stream=stream)
+    total = int(offs[-1].item())
+    out = torch.empty(max(total, 1), dtype=torch.uint8, device=buf.device)
+    N.gather(buf, off, length, out, offs, n, stream)
+    return out[:total], offs
+
+
+def xxh32_batch(src: torch.Tensor, off: torch.Tensor, length: torch.Tensor, seed: int = 0, stream=None):
+    """XXH32 of n device-resident items (uint32[n] as int64 tensor view)."""
+    n = off.numel()
+    out = torch.empty(n, dtype=torch.int32, device=src.device)
+    N.launch_xxh32_batch(src, off, length.to(torch.int64), seed, out, n, stream)
+    return out

@@ -1,0 +1,217 @@
+"""GPU parity of the HIP block codec against the CPU oracle (bit-exact).
+
+Everything here calls the HIP kernels through the C-ABI library
+(``lz4._native`` -> ``_lz4m.so``); the oracle (oracle/lz4_oracle.c, pinned to
+the reference by tests/test_oracle.py and tests/golden) is only the checker.
+"""
+import random
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from lz4 import _native as N
+from lz4 import _synth
+
+
+def _pack(blocks):
+    offs, lens, total = [], [], 0
+    for b in blocks:
+        offs.append(total)
+        lens.append(len(b))
+        total += len(b)
+    return b"".join(blocks), offs, lens
+
+
+def gpu_decompress(blocks, caps, dev):
+    packed, offs, lens = _pack(blocks)
+    d_src = N.to_device(packed, dev)
+    d_off, acc = [], 0
+    for c in caps:
+        d_off.append(acc)
+        acc += max(c, 0)
+    d_dst = torch.zeros(max(acc, 1), dtype=torch.uint8, device=dev)
+    st = torch.empty(len(blocks), dtype=torch.int32, device=dev)
+    N.launch_decompress(d_src, torch.tensor(offs, dtype=torch.int64, device=dev),
+                        torch.tensor(lens, dtype=torch.int32, device=dev), d_dst,
+                        torch.tensor(d_off, dtype=torch.int64, device=dev),
+                        torch.tensor(caps, dtype=torch.int32, device=dev), st, len(blocks))
+    host = d_dst.cpu().numpy()
+    out = []
+    for i, s in enumerate(st.cpu().tolist()):
+        out.append((s, host[d_off[i]:d_off[i] + s].tobytes() if s > 0 else b""))
+    return out
+
+
+def gpu_compress(blocks, table, dev, accel=1, caps=None):
+    packed, offs, lens = _pack(blocks)
+    caps = caps or [N.compress_bound(L) for L in lens]
+    d_src = N.to_device(packed, dev)
+    d_off, acc = [], 0
+    for c in caps:
+        d_off.append(acc)
+        acc += max(c, 1)
+    d_dst = torch.zeros(max(acc, 1), dtype=torch.uint8, device=dev)
+    ol = torch.empty(len(blocks), dtype=torch.int32, device=dev)
+    N.launch_compress(d_src, torch.tensor(offs, dtype=torch.int64, device=dev),
+                      torch.tensor(lens, dtype=torch.int32, device=dev), d_dst,
+                      torch.tensor(d_off, dtype=torch.int64, device=dev),
+                      torch.tensor(caps, dtype=torch.int32, device=dev), ol, len(blocks), table, accel)
+    host = d_dst.cpu().numpy()
+    return [host[d_off[i]:d_off[i] + L].tobytes() if L > 0 else None for i, L in enumerate(ol.cpu().tolist())]
+
+
+@pytest.fixture(scope="module")
+def corpus():
+    blocks = [b.tobytes() for b in _synth.blocks(96, "silesia", seed=11)]
+    rng = random.Random(5)
+    # ragged sizes, including every edge the format defines (0..13, 64K limit)
+    sizes = [0, 1, 4, 5, 11, 12, 13, 14, 15, 16, 17, 31, 32, 63, 64, 65, 100, 255, 256, 1000, 4095, 4096,
+             65535, 65536]
+    ragged = []
+    for s in sizes:
+        b = blocks[rng.randrange(len(blocks))]
+        ragged.append(b[:s])
+    return blocks, ragged
+
+
+def test_decompress_matches_oracle(gpu, oracle, corpus):
+    blocks, ragged = corpus
+    src = blocks + ragged + [bytes(65536), bytes([7]) * 65536, b"ab" * 32768]
+    comp = [oracle.compress(b) for b in src]
+    res = gpu_decompress(comp, [len(b) for b in src], gpu)
+    for i, (s, out) in enumerate(res):
+        assert s == len(src[i]), (i, s, len(src[i]))
+        assert out == src[i], i
+
+
+@pytest.mark.parametrize("variant", [N.TABLE_U16_HASH4, N.TABLE_U32_HASH5])
+def test_compress_bit_exact(gpu, oracle, corpus, variant):
+    blocks, ragged = corpus
+    src = blocks[:48] + ragged + [bytes(65536), bytes([7]) * 65536, b"ab" * 32768]
+    got = gpu_compress(src, variant, gpu)
+    for i, b in enumerate(src):
+        want = oracle.compress(b, variant)
+        assert got[i] == want, (i, len(b), None if got[i] is None else len(got[i]), len(want))
+
+
+def test_compress_acceleration(gpu, oracle, corpus):
+    blocks, _ = corpus
+    for accel in (2, 7, 100, 70000):
+        got = gpu_compress(blocks[:16], N.TABLE_U32_HASH5, gpu, accel=accel)
+        for i, b in enumerate(blocks[:16]):
+            assert got[i] == oracle.compress(b, N.TABLE_U32_HASH5, accel=accel), (accel, i)
+
+
+def test_compress_limited_output(gpu, oracle, corpus):
+    blocks, _ = corpus
+    src = blocks[:24]
+    caps = [len(b) - 1 for b in src]   # frame block capacity (lz4frame.c:835)
+    got = gpu_compress(src, N.TABLE_U16_HASH4, gpu, caps=caps)
+    for i, b in enumerate(src):
+        want = oracle.compress(b, N.TABLE_U16_HASH4, cap=caps[i])
+        assert got[i] == want, i
+
+
+def test_compress_large_block_u32(gpu, oracle, corpus):
+    blocks, _ = corpus
+    big = b"".join(blocks[:20])   # 1.25 MiB, byU32 with distance check
+    got = gpu_compress([big], N.TABLE_U32_HASH5, gpu)[0]
+    assert got == oracle.compress(big, N.TABLE_U32_HASH5)
+
+
+def test_decompress_malformed_matches_oracle(gpu, oracle, corpus):
+    blocks, _ = corpus
+    rng = random.Random(1234)
+    cases, caps = [], []
+    for _ in range(3000):
+        b = blocks[rng.randrange(len(blocks))]
+        n = rng.choice([20, 64, 100, 300, 2000, 65536])
+        off = rng.randrange(0, 65536 - n + 1)
+        c = bytearray(oracle.compress(b[off:off + n]))
+        for _ in range(rng.randrange(4)):
+            c[rng.randrange(len(c))] = rng.randrange(256)
+        if rng.random() < 0.2:
+            c = c[:rng.randrange(len(c) + 1)]
+        cases.append(bytes(c))
+        caps.append(rng.choice([n, n, n - 1, n + 1, n + 100, max(0, n - 20), 70, 0]))
+    res = gpu_decompress(cases, caps, gpu)
+    for i, (s, out) in enumerate(res):
+        want = oracle.decompress(cases[i], caps[i])
+        assert s == want[0], (i, s, want[0], caps[i])
+        if s >= 0:
+            assert out == want[1], i
+
+
+def test_decompress_random_garbage(gpu, oracle):
+    rng = np.random.default_rng(3)
+    cases = [rng.integers(0, 256, size=int(rng.integers(1, 300)), dtype=np.uint8).tobytes() for _ in range(2000)]
+    caps = [int(rng.integers(0, 5000)) for _ in cases]
+    res = gpu_decompress(cases, caps, gpu)
+    for i, (s, out) in enumerate(res):
+        want = oracle.decompress(cases[i], caps[i])
+        assert s == want[0], (i, s, want[0])
+        if s >= 0:
+            assert out == want[1]
+
+
+def test_decompress_dict(gpu, oracle, corpus):
+    blocks, _ = corpus
+    from lz4.block import decompress_many
+    d = blocks[0][:30000]
+    # build blocks that reference a dictionary: compress dict+data and strip
+    # the dictionary part is not possible with the plain compressor; instead
+    # check that dict-mode decode of ordinary blocks and of crafted blocks
+    # with offsets reaching into the dictionary matches the oracle.
+    crafted = []
+    for k in range(64):
+        lit = bytes([65 + k % 26]) * 3
+        off = 30 + k * 100
+        ml = 20 + k
+        seq = bytes([(3 << 4) | 15]) + lit + off.to_bytes(2, "little") + bytes([ml - 19])
+        tail = b"END__"
+        crafted.append(seq + bytes([len(tail) << 4]) + tail)
+    caps = [3 + 20 + k + 5 + 10 for k in range(64)]
+    res = decompress_many(crafted, uncompressed_size=caps, dict=d, raise_errors=False)
+    for i, c in enumerate(crafted):
+        s, want = oracle.decompress(c, caps[i], dict_=d)
+        if s < 0:
+            assert not isinstance(res[i], (bytes, bytearray))
+            assert str(-s) in str(res[i])
+        else:
+            assert res[i] == want, i
+
+
+def test_xxh32_batch(gpu, oracle, corpus):
+    blocks, ragged = corpus
+    items = blocks[:32] + ragged
+    packed, offs, lens = _pack(items)
+    d = N.to_device(packed, gpu)
+    out = torch.empty(len(items), dtype=torch.int32, device=gpu)
+    for seed in (0, 1, 0x9E3779B1):
+        N.launch_xxh32_batch(d, torch.tensor(offs, dtype=torch.int64, device=gpu),
+                             torch.tensor(lens, dtype=torch.int64, device=gpu), seed, out, len(items))
+        got = [v & 0xFFFFFFFF for v in out.cpu().tolist()]
+        assert got == [oracle.xxh32(b, seed) for b in items]
+
+
+@pytest.mark.parametrize("n", [0, 1, 15, 16, 17, 1023, 1024, 1025, 4096 + 7, 3 * 65536 + 5])
+def test_xxh32_long(gpu, oracle, corpus, n):
+    blocks, _ = corpus
+    data = (b"".join(blocks[:4]))[:n]
+    d = N.to_device(data, gpu, pad=1)
+    out = torch.empty(1, dtype=torch.int32, device=gpu)
+    N.launch_xxh32_long(d, n, 0, out)
+    assert out.item() & 0xFFFFFFFF == oracle.xxh32(data)
+
+
+def test_scan_and_gather(gpu):
+    rng = np.random.default_rng(0)
+    for n in (1, 5, 2047, 2048, 2049, 100000):
+        lens = rng.integers(0, 300, size=n).astype(np.int32)
+        t = torch.tensor(lens, device=gpu)
+        offs = N.exclusive_scan(t, add=3, base=11).cpu().numpy()
+        want = np.concatenate([[0], np.cumsum(lens.astype(np.int64) + 3)]) + 11
+        assert (offs == want).all(), n
