@@ -1,0 +1,276 @@
+"""Benchmark: batched LZ4 block codec on MI355X (BASELINE.json configs 2 and 3).
+
+One "step" = one pass of the hot path over one batch: decompress of
+1,048,576 x 64 KiB device-resident blocks (config 2, the headline `value`),
+plus the compress pass of the same batch (config 3) reported beside it.
+
+Data: the Silesia corpus is not available offline, so a seeded synthetic
+"silesia-like" mix (lz4/_synth.py) stands in.  A pool of unique blocks is
+generated on the host and tiled on the device with a per-tile XOR key (so
+every block is distinct in memory and no tile is served from cache), then
+compressed by our own compressor, which is byte-identical to
+LZ4_compress_default (tests/test_gpu_codec.py) -- i.e. the decompress input
+is exactly what lz4libs would produce.  Output is verified bit-exact against
+the original blocks at full size.
+
+Multi-GPU (torchrun, one process per GPU): every rank decodes its own
+1 M-block shard (weak scaling, no data-path collective); timing is the max
+over ranks between barriers.  value = all ranks' bytes / that time.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "python-lz4_amd"))
+
+from lz4 import _native as N  # noqa: E402
+from lz4 import _synth  # noqa: E402
+
+BLOCK = 65536
+GIB = float(1 << 30)
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def make_batch(n_blocks: int, pool: int, kind: str, seed: int, dev) -> torch.Tensor:
+    """n_blocks x 64 KiB on the device: a host-generated pool tiled with a
+    per-tile XOR key."""
+    host = _synth.blocks(pool, kind, seed=seed)
+    d_pool = torch.from_numpy(host).to(dev)
+    out = torch.empty((n_blocks, BLOCK), dtype=torch.uint8, device=dev)
+    tiles = (n_blocks + pool - 1) // pool
+    for t in range(tiles):
+        lo, hi = t * pool, min(n_blocks, (t + 1) * pool)
+        key = (t * 151 + 7) & 0xFF if t else 0
+        if key:
+            torch.bitwise_xor(d_pool[: hi - lo], key, out=out[lo:hi])
+        else:
+            out[lo:hi].copy_(d_pool[: hi - lo])
+    del d_pool
+    return out.view(-1)
+
+
+def compress_all(src: torch.Tensor, n: int, table: int, dev, events=None):
+    """Compress n blocks into bound-sized slots; returns slots, offsets, lengths."""
+    cap = N.compress_bound(BLOCK)
+    cap16 = (cap + 15) // 16 * 16
+    src_off = torch.arange(n, dtype=torch.int64, device=dev) * BLOCK
+    src_len = torch.full((n,), BLOCK, dtype=torch.int32, device=dev)
+    dst = torch.empty(n * cap16, dtype=torch.uint8, device=dev)
+    dst_off = torch.arange(n, dtype=torch.int64, device=dev) * cap16
+    dst_cap = torch.full((n,), cap, dtype=torch.int32, device=dev)
+    out_len = torch.empty(n, dtype=torch.int32, device=dev)
+    return (src_off, src_len, dst, dst_off, dst_cap, out_len)
+
+
+def time_kernel(fn, steps: int, warmup: int, world: int):
+    """Warmup, then time exactly `steps` calls bracketed by barrier+sync;
+    returns (wall seconds max over ranks, mean per-launch seconds from HIP
+    events recorded on the launch stream)."""
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    t0 = time.perf_counter()
+    for a, b in evs:
+        a.record()
+        fn()
+        b.record()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    ev_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    if world > 1:
+        t = torch.tensor([wall, ev_ms], dtype=torch.float64, device="cuda")
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        wall, ev_ms = float(t[0]), float(t[1])
+    return wall, ev_ms / 1e3
+
+
+def cpu_baseline(host_blocks: np.ndarray, comp_host: list, seconds: float = 10.0) -> dict:
+    """Reference lz4libs (oracle/_ref, compiled from /root/reference) on the
+    host cores: LZ4_decompress_safe over a bounded sample of the same
+    workload."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O   # test/bench infrastructure only
+    cb = O.CpuBench()
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    cores = max(1, min(cores, 16))   # the GPU box's CPU share is 16 cores
+    n = len(comp_host)
+    lens = np.array([len(c) for c in comp_host], dtype=np.int32)
+    src = np.frombuffer(b"".join(comp_host), dtype=np.uint8)
+    src_off = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
+    dst = np.empty(n * BLOCK, dtype=np.uint8)
+    dst_off = (np.arange(n, dtype=np.int64) * BLOCK)
+    dst_cap = np.full(n, BLOCK, dtype=np.int32)
+    secs, out = cb.run("decompress", cores, 1, src, src_off, lens, dst, dst_off, dst_cap)
+    reps = max(1, int(seconds / max(secs, 1e-3)))
+    secs, out = cb.run("decompress", cores, reps, src, src_off, lens, dst, dst_off, dst_cap)
+    assert (out == BLOCK).all(), "CPU baseline decode failed"
+    assert np.array_equal(dst.reshape(n, BLOCK), host_blocks[:n]), "CPU baseline output mismatch"
+    val = n * reps * BLOCK / secs / GIB
+    return {"value": round(val, 3), "unit": "GiB/s", "cores": cores, "kind": cb.kind,
+            "sample": f"LZ4_decompress_safe, {n} x 64 KiB silesia-like blocks x {reps} reps "
+                      f"({secs:.1f} s, {cores} pthreads, one contiguous slice each)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--blocks", type=int, default=1 << 20, help="64 KiB blocks per GPU (config 2: 1M)")
+    ap.add_argument("--pool", type=int, default=4096, help="unique host-generated blocks per rank")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-compress", action="store_true")
+    ap.add_argument("--random-blocks", type=int, default=1 << 17, help="blocks of the random-data extra line")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        torch.distributed.init_process_group("nccl", device_id=dev)
+    N.lib()
+
+    n = args.blocks
+    log(f"[bench] rank {rank}/{world}: generating {n} x 64 KiB silesia-like blocks (pool {args.pool})")
+    t_gen = time.perf_counter()
+    src = make_batch(n, args.pool, "silesia", seed=2026 + rank, dev=dev)
+    log(f"[bench] data ready in {time.perf_counter() - t_gen:.1f}s")
+
+    # ---- compress (config 3): LZ4_compress_default parse (byU16/hash4) ----
+    src_off, src_len, slots, slot_off, slot_cap, out_len = compress_all(src, n, N.TABLE_U16_HASH4, dev)
+
+    def do_compress():
+        N.launch_compress(src, src_off, src_len, slots, slot_off, slot_cap, out_len, n, N.TABLE_U16_HASH4, 1)
+
+    if args.no_compress:
+        do_compress()
+        c_wall, c_ev = float("nan"), float("nan")
+    else:
+        c_wall, c_ev = time_kernel(do_compress, max(1, args.steps // 2), 1, world)
+    assert int((out_len <= 0).sum()) == 0, "compress failed on some block"
+    comp_total = int(out_len.to(torch.int64).sum())
+    ratio = n * BLOCK / comp_total
+
+    # compact into one contiguous compressed buffer (what a file/socket holds)
+    offs = N.exclusive_scan(out_len)
+    comp = torch.empty(comp_total, dtype=torch.uint8, device=dev)
+    N.gather(slots, slot_off, out_len, comp, offs, n)
+    c_off = offs[:n].clone()
+    c_len = out_len.clone()
+    comp_sample = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        k = min(n, 16384)
+        comp_host_np = comp[: int(offs[k])].cpu().numpy()
+        oh = offs[: k + 1].cpu().numpy()
+        comp_sample = [comp_host_np[oh[i]:oh[i + 1]].tobytes() for i in range(k)]
+    del slots, slot_off, slot_cap
+    torch.cuda.empty_cache()
+
+    # ---- decompress (config 2, headline) ----
+    dst = torch.empty(n * BLOCK, dtype=torch.uint8, device=dev)
+    dst_off = torch.arange(n, dtype=torch.int64, device=dev) * BLOCK
+    dst_cap = torch.full((n,), BLOCK, dtype=torch.int32, device=dev)
+    status = torch.empty(n, dtype=torch.int32, device=dev)
+
+    def do_decompress():
+        N.launch_decompress(comp, c_off, c_len, dst, dst_off, dst_cap, status, n)
+
+    d_wall, d_ev = time_kernel(do_decompress, args.steps, args.warmup, world)
+    ok_status = bool((status == BLOCK).all())
+    ok_bytes = bool(torch.equal(dst, src))
+    if not (ok_status and ok_bytes):
+        raise SystemExit(f"decompress verification failed: status_ok={ok_status} bytes_ok={ok_bytes}")
+
+    # ---- extra: incompressible (random) blocks ----
+    extra = {}
+    if args.random_blocks > 0:
+        del dst
+        torch.cuda.empty_cache()
+        nr = min(args.random_blocks, n)
+        rsrc = make_batch(nr, min(args.pool, nr), "random", seed=99 + rank, dev=dev)
+        r_off, r_len, r_slots, r_soff, r_scap, r_olen = compress_all(rsrc, nr, N.TABLE_U16_HASH4, dev)
+        N.launch_compress(rsrc, r_off, r_len, r_slots, r_soff, r_scap, r_olen, nr, N.TABLE_U16_HASH4, 1)
+        rdst = torch.empty(nr * BLOCK, dtype=torch.uint8, device=dev)
+        rst = torch.empty(nr, dtype=torch.int32, device=dev)
+
+        def do_rand():
+            N.launch_decompress(r_slots, r_soff, r_olen, rdst, dst_off[:nr], dst_cap[:nr], rst, nr)
+
+        r_wall, r_ev = time_kernel(do_rand, args.steps, 1, world)
+        assert bool(torch.equal(rdst, rsrc)), "random-data round trip failed"
+        r_cbytes = int(r_olen.to(torch.int64).sum())
+        extra["decompress_random_gib_s"] = round(world * nr * BLOCK / (r_wall / args.steps) / GIB, 2)
+        extra["decompress_random_kernel_gbs"] = round((r_cbytes + nr * BLOCK) / r_ev / 1e9, 1)
+
+    # ---- report ----
+    d_step = d_wall / args.steps
+    value = world * n * BLOCK / d_step / GIB
+    algo_bytes = comp_total + n * BLOCK          # per launch: read compressed + write decoded
+    achieved = algo_bytes / d_ev / 1e9           # GB/s, from HIP events on the launch stream
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_decompress.json")
+    if os.path.exists(pmc_path):
+        try:
+            with open(pmc_path) as f:
+                traffic = json.load(f).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    res = {
+        "metric": "GiB/s uncompressed, device-resident, 64 KiB blocks (decompress; compress)",
+        "value": round(value, 2),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(d_step * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (silesia-like mix, lz4/_synth.py; Silesia unavailable offline)",
+        "config": {"workload": "config 2: decompress 1M x 64 KiB blocks, device-resident, LZ4_compress_default input",
+                   "blocks_per_gpu": n, "block_size": BLOCK, "ratio": round(ratio, 4),
+                   "parallelism": f"shard{world}"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic},
+        "compress_gib_s": None if c_wall != c_wall else round(world * n * BLOCK / (c_wall / max(1, args.steps // 2)) / GIB, 2),
+        "compress_kernel_ms": None if c_ev != c_ev else round(c_ev * 1e3, 3),
+        "decompress_kernel_ms": round(d_ev * 1e3, 3),
+        "extra": extra,
+    }
+    if comp_sample is not None:
+        host_blocks = src[: len(comp_sample) * BLOCK].view(-1, BLOCK).cpu().numpy()
+        res["cpu_baseline"] = cpu_baseline(host_blocks, comp_sample)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

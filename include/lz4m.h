@@ -76,6 +76,18 @@ int lz4m_decompress_batch_dict(const uint8_t* d_src, const int64_t* d_src_off, c
                                int32_t* d_status, int64_t n, lz4m_stream_t stream);
 
 /*
+ * Linked-block frame decode (LZ4F_decompress on a blockLinked frame,
+ * lz4frame.c:1844-1856): block i may reference the output of blocks < i, so
+ * blocks decode in order on one wavefront, contiguously into d_dst (capacity
+ * max_block per block).  d_raw_flag[i] != 0 marks a stored (uncompressed)
+ * block, copied as is.  d_status[i] = decoded size or -(pos)-1; after the
+ * first failing block the remaining statuses are -1.
+ */
+int lz4m_decompress_chain(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len,
+                          const uint8_t* d_raw_flag, uint8_t* d_dst, int32_t* d_status, int64_t n,
+                          int32_t max_block, lz4m_stream_t stream);
+
+/*
  * Batched greedy compressor, bit-exact with the reference parse for the
  * chosen table layout (LZ4_compress_generic_validated, lz4.c:910-1302, fresh
  * table per block).  acceleration as LZ4_compress_fast (clamped to

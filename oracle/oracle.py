@@ -228,3 +228,39 @@ class CpuBench:
         secs = self.lib.cpu_bench_run(code, threads, reps, ptr(src), ptr(src_off), ptr(src_len),
                                       ptr(dst), ptr(dst_off), ptr(dst_cap), ptr(out), src_off.size)
         return secs, out
+
+
+def ref_decompress_frame(ref: "Reference", data: bytes) -> tuple[int, bytes]:
+    """Decode one frame with the reference LZ4F_decompress (test helper).
+    Returns (error code or 0, decoded bytes)."""
+    lib = ref.lib
+    vp, sz = C.c_void_p, C.c_size_t
+    lib.LZ4F_createDecompressionContext.argtypes = [C.POINTER(vp), C.c_uint]
+    lib.LZ4F_createDecompressionContext.restype = sz
+    lib.LZ4F_freeDecompressionContext.argtypes = [vp]
+    lib.LZ4F_decompress.argtypes = [vp, vp, C.POINTER(sz), vp, C.POINTER(sz), vp]
+    lib.LZ4F_decompress.restype = sz
+    lib.LZ4F_getErrorName.argtypes = [sz]
+    lib.LZ4F_getErrorName.restype = C.c_char_p
+    ctx = vp()
+    lib.LZ4F_createDecompressionContext(C.byref(ctx), 100)
+    src = np.frombuffer(bytes(data), dtype=np.uint8)
+    out = bytearray()
+    pos = 0
+    buf = np.zeros(1 << 23, dtype=np.uint8)
+    try:
+        while True:
+            dsz = sz(buf.size)
+            ssz = sz(src.size - pos)
+            r = lib.LZ4F_decompress(ctx, buf.ctypes.data_as(vp), C.byref(dsz),
+                                    (src.ctypes.data + pos) if src.size else None, C.byref(ssz), None)
+            out += buf[:dsz.value].tobytes()
+            pos += ssz.value
+            if lib.LZ4F_isError(r):
+                return -1, lib.LZ4F_getErrorName(r).decode()
+            if r == 0:
+                return 0, bytes(out)
+            if pos >= src.size and dsz.value == 0:
+                return 1, bytes(out)
+    finally:
+        lib.LZ4F_freeDecompressionContext(ctx)

@@ -421,6 +421,86 @@ __global__ __launch_bounds__(256) void decompress_kernel(const uint8_t* __restri
     if (i < n) status[i] = L.result;
 }
 
+
+// Linked-block frames (lz4frame.c:1853-1856, LZ4F_updateDict): block i may
+// reference the output of blocks < i, so the chain decodes in order on one
+// wavefront, contiguously into dst.  Lane 0 parses; the wave runs the long
+// copies.  Prefix semantics = LZ4_decompress_safe_usingDict with the
+// previous output as a contiguous prefix (withSmallPrefix / withPrefix64k,
+// lz4.c:2612-2625): offsets may reach min(prefix, 64 KiB) before the block.
+__global__ __launch_bounds__(64) void decompress_chain_kernel(const uint8_t* __restrict__ src,
+                                                              const int64_t* __restrict__ src_off,
+                                                              const int32_t* __restrict__ src_len,
+                                                              const uint8_t* __restrict__ raw_flag, uint8_t* dst,
+                                                              int32_t* __restrict__ status, int64_t n,
+                                                              int32_t max_block) {
+    const uint32_t lane = threadIdx.x;
+    int64_t running = 0;
+    for (int64_t b = 0; b < n; ++b) {
+        const int64_t len = src_len[b];
+        const uint8_t* s = src + src_off[b];
+        uint8_t* d = dst + running;
+        if (raw_flag[b]) {
+            wave_literal(d, s, len, len, len, lane);
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            if (lane == 0) status[b] = (int32_t)len;
+            running += len;
+            continue;
+        }
+        Lane L;
+        L.live = false;
+        L.result = -1;
+        if (lane == 0) {
+            L.src = s;
+            L.dst = d;
+            L.iend = len;
+            L.oend = max_block;
+            L.ip = 0;
+            L.op = 0;
+            L.dict_len = running < 65536 ? running : 65536;
+            L.dict_end = d;
+            if (L.iend <= 0) {
+                L.result = -1;
+            } else {
+                L.fast = L.oend >= 64;
+                L.live = true;
+            }
+        }
+        while (__any(L.live)) {
+            Copy lc{kNone, 0, 0, 0}, mc{kNone, 0, 0, 0};
+            if (L.live) decode_step<true>(L, lc, mc);
+            const uint64_t pend = __ballot(lc.kind != kNone || mc.kind != kNone);
+            if (pend == 0) continue;
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            uint8_t* dd = readlane_ptr(L.dst, 0);
+            const int64_t oend = readlane64(L.oend, 0);
+            if (__builtin_amdgcn_readlane(lc.kind, 0) != kNone) {
+                const uint8_t* ss = readlane_ptr(L.src, 0);
+                const int64_t iend = readlane64(L.iend, 0);
+                const int64_t dp = readlane64(lc.dpos, 0), sp = readlane64(lc.arg, 0), ln = readlane64(lc.len, 0);
+                wave_literal(dd + dp, ss + sp, ln, oend - dp, iend - sp, lane);
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            }
+            if (__builtin_amdgcn_readlane(mc.kind, 0) != kNone) {
+                const int64_t dp = readlane64(mc.dpos, 0), off = readlane64(mc.arg, 0), ln = readlane64(mc.len, 0);
+                if (off < 0) {
+                    if (lane == 0) dict_match(L, dp, -off, ln);
+                } else {
+                    wave_match(dd + dp, off, ln, oend - dp, lane);
+                }
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            }
+        }
+        const int32_t r = __builtin_amdgcn_readlane(L.result, 0);
+        if (lane == 0) status[b] = r;
+        if (r < 0) {
+            for (int64_t k = b + 1 + lane; k < n; k += kWave) status[k] = -1;
+            return;
+        }
+        running += r;
+    }
+}
+
 }  // namespace lz4m
 
 using namespace lz4m;
@@ -447,5 +527,15 @@ extern "C" int lz4m_decompress_batch_dict(const uint8_t* d_src, const int64_t* d
     hipLaunchKernelGGL(decompress_kernel<true>, dim3((uint32_t)grid), dim3(256), 0, (hipStream_t)stream, d_src,
                        d_src_off, d_src_len, d_dst, d_dst_off, d_dst_cap, d_dict, d_dict_off, d_dict_len, d_status,
                        n);
+    return (int)hipGetLastError();
+}
+
+extern "C" int lz4m_decompress_chain(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len,
+                                     const uint8_t* d_raw_flag, uint8_t* d_dst, int32_t* d_status, int64_t n,
+                                     int32_t max_block, lz4m_stream_t stream) {
+    if (n < 0 || max_block < 0) return LZ4M_EINVAL;
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(decompress_chain_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, d_src, d_src_off,
+                       d_src_len, d_raw_flag, d_dst, d_status, n, max_block);
     return (int)hipGetLastError();
 }

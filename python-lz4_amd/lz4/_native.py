@@ -35,6 +35,7 @@ def _declare(lib) -> None:
         "lz4m_version_string": ([], C.c_char_p),
         "lz4m_decompress_batch": ([vp, vp, vp, vp, vp, vp, vp, i64, vp], i32),
         "lz4m_decompress_batch_dict": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, vp], i32),
+        "lz4m_decompress_chain": ([vp, vp, vp, vp, vp, vp, i64, i32, vp], i32),
         "lz4m_compress_batch": ([vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, vp], i32),
         "lz4m_xxh32_batch": ([vp, vp, vp, u32, vp, i64, vp], i32),
         "lz4m_xxh32_long": ([vp, i64, u32, vp, vp], i32),
@@ -104,6 +105,13 @@ def launch_decompress(src, src_off, src_len, dst, dst_off, dst_cap, status, n, s
                                           ptr(dst_cap), ptr(dict_buf), ptr(dict_off), ptr(dict_len), ptr(status),
                                           n, sp)
     check(rc, "lz4m_decompress_batch")
+
+
+def launch_decompress_chain(src, src_off, src_len, raw_mask, dst, status, n, max_block, stream=None) -> None:
+    raw = raw_mask.to(torch.uint8)
+    rc = lib().lz4m_decompress_chain(ptr(src), ptr(src_off), ptr(src_len), ptr(raw), ptr(dst), ptr(status), n,
+                                     max_block, stream_ptr(stream))
+    check(rc, "lz4m_decompress_chain")
 
 
 def launch_compress(src, src_off, src_len, dst, dst_off, dst_cap, out_len, n, table, accel, stream=None) -> None:

@@ -1,0 +1,342 @@
+"""``lz4.frame`` one-shot API on the MI355X codec.
+
+Mirrors the reference extension ``lz4/frame/_frame.c`` (compress 112-259,
+get_frame_info 640-824, __decompress 938-1193) over the frame format of
+``lz4libs/lz4frame.c``.  The host walks the frame structure (header bytes,
+LE32 block records); every byte-level operation runs on the GPU:
+
+* compress: the input is cut into blocks and compressed in one batched
+  launch with the LZ4_compress_fast_extState_fastReset parse
+  (lz4frame.c:853-863 -> lz4.c:1378-1413, cap = block size - 1, raw block when
+  it does not fit, lz4frame.c:834-842); block records are emitted by
+  ``lz4m_frame_emit`` at scanned offsets; the header checksum and the content
+  checksum (XXH32, lz4frame.c:341-345, 1042, 1171) run on the device.
+* decompress: independent blocks decode in one batched launch into slots of
+  the frame's maximum block size (the capacity LZ4F_decompress gives,
+  lz4frame.c:1844-1847), raw blocks are gathered, block checksums and the
+  content checksum are verified on the device.  Linked-block frames decode
+  block after block on one wavefront with the previous output as prefix.
+
+Scope notes: ``block_linked=True`` frames are written with the
+linked flag but independently compressed blocks -- a valid frame that every
+decoder accepts, a little larger than the reference's at 64 KiB blocks; HC
+levels (>= 3) and the chunked / context streaming API are outside this
+codec's scope.
+"""
+from __future__ import annotations
+
+import struct
+
+import torch
+
+from .. import _native as N
+from ..block._block import _buffer, _c_int
+
+BLOCKSIZE_DEFAULT = 0
+BLOCKSIZE_MAX64KB = 4
+BLOCKSIZE_MAX256KB = 5
+BLOCKSIZE_MAX1MB = 6
+BLOCKSIZE_MAX4MB = 7
+
+_MAGIC = 0x184D2204
+_MAGIC_SKIPPABLE = 0x184D2A50
+_BLOCK_SIZES = {4: 64 << 10, 5: 256 << 10, 6: 1 << 20, 7: 4 << 20}
+_MIN_FH = 7        # lz4frame.c minFHSize
+_BH = 4            # block header size
+_UNCOMPRESSED = 0x80000000
+
+
+def _err(fn: str, code: str) -> RuntimeError:
+    return RuntimeError(f"{fn} failed with code: ERROR_{code}")
+
+
+def _xxh32_dev(buf: bytes | memoryview | torch.Tensor, n: int | None = None, seed: int = 0) -> int:
+    dev = N.device()
+    t = buf if isinstance(buf, torch.Tensor) else N.to_device(buf, dev, pad=1)
+    length = n if n is not None else (t.numel() if isinstance(buf, torch.Tensor) else memoryview(buf).nbytes)
+    out = torch.empty(1, dtype=torch.int32, device=t.device)
+    N.launch_xxh32_long(t, length, seed, out)
+    return int(out.item()) & 0xFFFFFFFF
+
+
+# ------------------------------------------------------------------ header
+def _optimal_bsid(requested: int, size: int) -> int:
+    """LZ4F_optimalBSID (lz4frame.c:351-363)."""
+    proposed, max_size = 4, 64 << 10
+    while requested > proposed:
+        if size <= max_size:
+            return proposed
+        proposed += 1
+        max_size <<= 2
+    return requested
+
+
+def _header(bsid: int, linked: bool, block_checksum: bool, content_size: int, content_checksum: bool) -> bytes:
+    """LZ4F_compressBegin_usingCDict header (lz4frame.c:752-780)."""
+    flg = (1 << 6) | ((0 if linked else 1) << 5) | (int(block_checksum) << 4) \
+        | (int(content_size > 0) << 3) | (int(content_checksum) << 2)
+    body = bytes([flg, (bsid & 7) << 4])
+    if content_size:
+        body += struct.pack("<Q", content_size)
+    hc = (_xxh32_dev(body) >> 8) & 0xFF
+    return struct.pack("<I", _MAGIC) + body + bytes([hc])
+
+
+def _parse_header(mv: memoryview):
+    """LZ4F_getFrameInfo -> LZ4F_headerSize + LZ4F_decodeHeader
+    (lz4frame.c:1291-1380, 1387-1463).  Returns (info dict, header size)."""
+    fn = "LZ4F_getFrameInfo"
+    n = mv.nbytes
+    if n < 5:
+        raise _err(fn, "frameHeader_incomplete")
+    magic = struct.unpack_from("<I", mv, 0)[0]
+    if (magic & 0xFFFFFFF0) == _MAGIC_SKIPPABLE:
+        if n < 8:
+            raise _err(fn, "frameHeader_incomplete")
+        return {"skippable": True, "frame_size": struct.unpack_from("<I", mv, 4)[0]}, 8
+    if magic != _MAGIC:
+        raise _err(fn, "frameType_unknown")
+    flg = mv[4]
+    hsize = _MIN_FH + (8 if flg & 0x08 else 0) + (4 if flg & 0x01 else 0)
+    if n < hsize:
+        raise _err(fn, "frameHeader_incomplete")
+    if (flg >> 1) & 1:
+        raise _err(fn, "reservedFlag_set")
+    if (flg >> 6) & 3 != 1:
+        raise _err(fn, "headerVersion_wrong")
+    bd = mv[5]
+    bsid = (bd >> 4) & 7
+    if (bd >> 7) & 1:
+        raise _err(fn, "reservedFlag_set")
+    if bsid < 4:
+        raise _err(fn, "maxBlockSize_invalid")
+    if bd & 0x0F:
+        raise _err(fn, "reservedFlag_set")
+    hc = (_xxh32_dev(bytes(mv[4:hsize - 1])) >> 8) & 0xFF
+    if hc != mv[hsize - 1]:
+        raise _err(fn, "headerChecksum_invalid")
+    info = {
+        "skippable": False,
+        "block_size_id": bsid,
+        "block_size": _BLOCK_SIZES[bsid],
+        "block_linked": not bool((flg >> 5) & 1),
+        "block_checksum": bool((flg >> 4) & 1),
+        "content_checksum": bool((flg >> 2) & 1),
+        "content_size": struct.unpack_from("<Q", mv, 6)[0] if flg & 0x08 else 0,
+        "dict_id": struct.unpack_from("<I", mv, hsize - 5)[0] if flg & 0x01 else 0,
+    }
+    return info, hsize
+
+
+def get_frame_info(data):
+    """get_frame_info(data) -- frame parameters of the frame at the start of
+    data (_frame.c:640-824)."""
+    mv = _buffer(data)
+    info, _ = _parse_header(mv)
+    if info["skippable"]:
+        return {"block_size": 64 << 10, "block_size_id": BLOCKSIZE_MAX64KB, "block_linked": True,
+                "content_checksum": False, "block_checksum": False, "skippable": True, "content_size": 0}
+    return {k: info[k] for k in ("block_size", "block_size_id", "block_linked", "content_checksum",
+                                  "block_checksum", "skippable", "content_size")}
+
+
+# ---------------------------------------------------------------- compress
+def compress(data, compression_level=0, block_size=0, content_checksum=False, block_checksum=False,
+             block_linked=True, store_size=True, return_bytearray=False):
+    """compress(data, compression_level=0, block_size=0, content_checksum=0,
+    block_checksum=0, block_linked=True, store_size=True,
+    return_bytearray=False) -- one LZ4 frame (_frame.c:112-259 ->
+    LZ4F_compressFrame, lz4frame.c:420-515)."""
+    src = _buffer(data, "data")
+    level = _c_int(compression_level, "compression_level")
+    bsid_req = _c_int(block_size, "block_size")
+    if level >= 3:
+        raise NotImplementedError("LZ4 HC compression levels (>= 3) are outside the MI355X codec's scope")
+    accel = -level + 1 if level < 0 else 1                     # lz4frame.c:855
+    n = src.nbytes
+    bsid = _optimal_bsid(bsid_req, n)
+    if bsid == 0:
+        bsid = BLOCKSIZE_MAX64KB                               # LZ4F_BLOCKSIZEID_DEFAULT
+    if bsid not in _BLOCK_SIZES:
+        raise RuntimeError("LZ4F_compressFrame failed with code: ERROR_maxBlockSize_invalid")
+    bsize = _BLOCK_SIZES[bsid]
+    linked = bool(block_linked) and n > bsize                  # lz4frame.c:441-442
+    content_size = n if store_size else 0
+    hdr = _header(bsid, linked, bool(block_checksum), content_size, bool(content_checksum))
+
+    dev = N.device()
+    d_src = N.to_device(src, dev, pad=1)
+    nb = (n + bsize - 1) // bsize
+    parts = [hdr]
+    if nb:
+        raw_off = torch.arange(nb, dtype=torch.int64, device=dev) * bsize
+        raw_len = torch.full((nb,), bsize, dtype=torch.int32, device=dev)
+        raw_len[-1] = n - (nb - 1) * bsize
+        cap = raw_len - 1                                      # lz4frame.c:835: dstCapacity = srcSize - 1
+        slot = N.compress_bound(bsize)
+        cmp = torch.empty(nb * slot, dtype=torch.uint8, device=dev)
+        cmp_off = torch.arange(nb, dtype=torch.int64, device=dev) * slot
+        cmp_len = torch.empty(nb, dtype=torch.int32, device=dev)
+        N.launch_compress(d_src, raw_off, raw_len, cmp, cmp_off, cap, cmp_len, nb, N.TABLE_AUTO, accel)
+        rec_len = torch.empty(nb, dtype=torch.int32, device=dev)
+        N.frame_block_sizes(raw_len, cmp_len, block_checksum, rec_len, nb)
+        frame_off = N.exclusive_scan(rec_len)
+        total = int(frame_off[-1].item())
+        body = torch.empty(total + 16, dtype=torch.uint8, device=dev)
+        N.frame_emit(d_src, raw_off, raw_len, cmp, cmp_off, cmp_len, body, frame_off, block_checksum, nb)
+        parts.append(body[:total].cpu().numpy().tobytes())
+    parts.append(b"\x00\x00\x00\x00")                          # endmark, lz4frame.c:1167
+    if content_checksum:
+        parts.append(struct.pack("<I", _xxh32_dev(d_src, n)))  # lz4frame.c:1170-1176
+    out = b"".join(parts)
+    return bytearray(out) if return_bytearray else out
+
+
+# -------------------------------------------------------------- decompress
+def _scan_blocks(mv: memoryview, pos: int, info: dict):
+    """Walk the block records the way LZ4F_decompress consumes them
+    (lz4frame.c:1643-1701, 1926-1965).  Returns (records, end_state) where
+    records = [(raw, data_pos, size, crc_pos)] and end_state is either
+    ("end", bytes_read) or ("incomplete", hint) or ("error", code, index)."""
+    n = mv.nbytes
+    crc = 4 if info["block_checksum"] else 0
+    maxb = info["block_size"]
+    recs = []
+    while True:
+        if n - pos < _BH:
+            return recs, ("incomplete", _BH - (n - pos))
+        hdr = struct.unpack_from("<I", mv, pos)[0]
+        pos += _BH
+        if hdr == 0:                                           # endmark
+            if info["content_checksum"]:
+                if n - pos < 4:
+                    return recs, ("incomplete_suffix", 4 - (n - pos), pos)
+                return recs, ("end", pos + 4, pos)
+            return recs, ("end", pos, None)
+        size = hdr & 0x7FFFFFFF
+        if size > maxb:
+            return recs, ("error", "maxBlockSize_invalid", len(recs))
+        raw = bool(hdr & _UNCOMPRESSED)
+        avail = n - pos
+        if raw:
+            if avail < size + crc:
+                got = min(avail, size)
+                if avail <= size:
+                    hint = (size - got) + crc + _BH
+                else:
+                    hint = crc - (avail - size) + _BH
+                return recs, ("incomplete", hint if avail else _BH + size + crc)
+        elif avail < size + crc:
+            hint = (size + crc - avail) + crc + _BH if avail else _BH + size + crc
+            return recs, ("incomplete", hint)
+        recs.append((raw, pos, size, pos + size if crc else -1))
+        pos += size + crc
+
+
+def decompress(data, return_bytearray=False, return_bytes_read=False):
+    """decompress(data, return_bytearray=False, return_bytes_read=False) --
+    decode one full frame (_frame.c:1198-1258 -> __decompress 938-1193)."""
+    mv = _buffer(data, "data")
+    info, hsize = _parse_header(mv)
+    if info["skippable"]:
+        end = min(mv.nbytes, hsize + info["frame_size"])
+        if mv.nbytes < hsize + info["frame_size"]:
+            raise RuntimeError(f"Frame incomplete. LZ4F_decompress returned: {hsize + info['frame_size'] - mv.nbytes}")
+        out = bytearray() if return_bytearray else b""
+        return (out, end) if return_bytes_read else out
+    recs, state = _scan_blocks(mv, hsize, info)
+    dec = "LZ4F_decompress"
+    dev = N.device()
+    nb = len(recs)
+    maxb = info["block_size"]
+    out_t = None
+    total = 0
+    first_err = None          # (block index, code)
+    if nb:
+        d_frame = N.to_device(mv, dev, pad=16)
+        cpos = [r[1] for r in recs]
+        clen = [r[2] for r in recs]
+        is_raw = [r[0] for r in recs]
+        # block checksums (of the stored payload), verified first per block
+        crc_bad = [False] * nb
+        if info["block_checksum"]:
+            sums = torch.empty(nb, dtype=torch.int32, device=dev)
+            N.launch_xxh32_batch(d_frame, torch.tensor(cpos, dtype=torch.int64, device=dev),
+                                 torch.tensor(clen, dtype=torch.int64, device=dev), 0, sums, nb)
+            got = [v & 0xFFFFFFFF for v in sums.cpu().tolist()]
+            for i, r in enumerate(recs):
+                if got[i] != struct.unpack_from("<I", mv, r[3])[0]:
+                    crc_bad[i] = True
+        slots = torch.empty(nb * maxb + 16, dtype=torch.uint8, device=dev)
+        slot_off = torch.arange(nb, dtype=torch.int64, device=dev) * maxb
+        c_off = torch.tensor(cpos, dtype=torch.int64, device=dev)
+        c_len = torch.tensor(clen, dtype=torch.int32, device=dev)
+        raw_mask = torch.tensor(is_raw, dtype=torch.bool, device=dev)
+        status = torch.empty(nb, dtype=torch.int32, device=dev)
+        caps = torch.full((nb,), maxb, dtype=torch.int32, device=dev)
+        if info["block_linked"] and nb > 1 and not all(is_raw):
+            _decode_linked(d_frame, c_off, c_len, raw_mask, slots, status, maxb)
+            sizes = status.cpu().tolist()
+            dst_off_list = None
+        else:
+            # raw blocks are handed to the decoder with length 0 (immediate
+            # reject, no work); they are gathered from the frame below
+            dec_len = torch.where(raw_mask, torch.zeros_like(c_len), c_len)
+            N.launch_decompress(d_frame, c_off, dec_len, slots, slot_off, caps, status, nb)
+            sizes = status.cpu().tolist()
+            for i in range(nb):
+                if is_raw[i]:
+                    sizes[i] = clen[i]
+            dst_off_list = None
+        for i in range(nb):
+            if crc_bad[i]:
+                first_err = (i, "blockChecksum_invalid")
+                break
+            if not is_raw[i] and sizes[i] < 0:
+                first_err = (i, "decompressionFailed")
+                break
+        if first_err is None:
+            if info["block_linked"] and nb > 1 and not all(is_raw):
+                total = sum(sizes)
+                out_t = slots                                  # already contiguous
+            else:
+                lens = torch.tensor(sizes, dtype=torch.int32, device=dev)
+                src_off = torch.where(raw_mask, c_off, slot_off)
+                src_buf_is_frame = raw_mask
+                offs = N.exclusive_scan(lens)
+                total = int(offs[-1].item())
+                out_t = torch.empty(total + 16, dtype=torch.uint8, device=dev)
+                # compressed blocks from the slots, raw blocks from the frame
+                sel_c = torch.nonzero(~src_buf_is_frame).flatten()
+                sel_r = torch.nonzero(src_buf_is_frame).flatten()
+                if sel_c.numel():
+                    N.gather(slots, slot_off[sel_c], lens[sel_c], out_t, offs[sel_c], sel_c.numel())
+                if sel_r.numel():
+                    N.gather(d_frame, c_off[sel_r], lens[sel_r], out_t, offs[sel_r], sel_r.numel())
+    if first_err is not None:
+        raise _err(dec, first_err[1])
+    if state[0] == "error":
+        raise _err(dec, state[1])
+    if state[0] == "incomplete":
+        raise RuntimeError(f"Frame incomplete. LZ4F_decompress returned: {state[1]}")
+    if info["content_size"] and total != info["content_size"]:
+        raise _err(dec, "frameSize_wrong")                     # lz4frame.c:1927
+    if state[0] == "incomplete_suffix":
+        raise RuntimeError(f"Frame incomplete. LZ4F_decompress returned: {state[1]}")
+    bytes_read = state[1]
+    if info["content_checksum"]:
+        want = struct.unpack_from("<I", mv, state[2])[0]
+        got = _xxh32_dev(out_t, total) if total else _xxh32_dev(b"")
+        if got != want:
+            raise _err(dec, "contentChecksum_invalid")
+    out = N.to_host_bytes(out_t, total, bool(return_bytearray)) if total else (bytearray() if return_bytearray else b"")
+    if return_bytes_read:
+        return out, bytes_read
+    return out
+
+
+def _decode_linked(d_frame, c_off, c_len, raw_mask, out, status, maxb):
+    """Linked blocks: each block may reference the previous output
+    (LZ4F_updateDict, lz4frame.c:1853-1856), so blocks decode in order on one
+    wavefront, contiguously into `out`."""
+    N.launch_decompress_chain(d_frame, c_off, c_len, raw_mask, out, status, c_off.numel(), maxb)

@@ -1,0 +1,88 @@
+"""CPU tests of the drop-in boundary: the C-ABI library loads and exports
+every symbol include/lz4m.h declares; argument checks that need no GPU."""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "lz4m.h")
+
+
+def declared_symbols():
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:[\w\s\*]+?)\b(lz4m_\w+)\s*\(", txt, re.M)))
+
+
+def test_header_declares_entry_points():
+    syms = declared_symbols()
+    for s in ["lz4m_decompress_batch", "lz4m_decompress_batch_dict", "lz4m_decompress_chain",
+              "lz4m_compress_batch", "lz4m_xxh32_batch", "lz4m_xxh32_long", "lz4m_compress_bound",
+              "lz4m_exclusive_scan", "lz4m_gather", "lz4m_frame_emit", "lz4m_frame_block_sizes"]:
+        assert s in syms, s
+
+
+def test_library_exports_every_declared_symbol():
+    from lz4 import _native as N
+    lib = N.lib()
+    for s in declared_symbols():
+        assert hasattr(lib, s), f"{s} declared in include/lz4m.h but not exported"
+
+
+def test_compress_bound_and_version():
+    from lz4 import _native as N
+    lib = N.lib()
+    for n in [0, 1, 255, 65536, 1 << 20, 0x7E000000]:
+        assert lib.lz4m_compress_bound(n) == n + n // 255 + 16
+    assert lib.lz4m_compress_bound(0x7E000001) == 0
+    assert lib.lz4m_compress_bound(-1) == 0
+    assert lib.lz4m_version_number() == 10904
+
+
+def test_argument_validation_without_gpu():
+    """n == 0 is a no-op and n < 0 is rejected before any HIP call."""
+    from lz4 import _native as N
+    lib = N.lib()
+    assert lib.lz4m_decompress_batch(None, None, None, None, None, None, None, 0, None) == 0
+    assert lib.lz4m_decompress_batch(None, None, None, None, None, None, None, -1, None) == N.EINVAL
+    assert lib.lz4m_compress_batch(None, None, None, None, None, None, None, 0, 0, 1, None) == 0
+    assert lib.lz4m_compress_batch(None, None, None, None, None, None, None, -5, 0, 1, None) == N.EINVAL
+    assert lib.lz4m_xxh32_batch(None, None, None, 0, None, -1, None) == N.EINVAL
+    assert lib.lz4m_xxh32_long(None, -1, 0, None, None) == N.EINVAL
+
+
+def test_no_cpu_fallback():
+    """Without a HIP device every compute entry point raises (no silent CPU path)."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    import lz4.block
+    import lz4.frame
+    with pytest.raises(RuntimeError, match="no HIP device"):
+        lz4.block.compress(b"abc" * 100)
+    with pytest.raises(RuntimeError, match="no HIP device"):
+        lz4.block.decompress(b"\x01\x00\x00\x00\x10 ")
+    with pytest.raises(RuntimeError, match="no HIP device"):
+        lz4.frame.compress(b"abc")
+
+
+def test_package_does_not_import_oracle():
+    pkg = os.path.join(ROOT, "python-lz4_amd", "lz4")
+    for dirpath, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith(".py"):
+                src = open(os.path.join(dirpath, f)).read()
+                assert "import oracle" not in src and "liboracle" not in src and "libref_" not in src, f
+
+
+def test_block_api_argument_errors_without_gpu():
+    """Argument checks of _block.c that happen before any codec call."""
+    import lz4.block
+    with pytest.raises(TypeError):
+        lz4.block.compress("a str")
+    with pytest.raises(OverflowError):
+        lz4.block.decompress(b"abcd", uncompressed_size=(1 << 32) + 64)
+    with pytest.raises(ValueError, match="Invalid mode argument"):
+        lz4.block.compress(b"x", mode="nope")

@@ -1,0 +1,276 @@
+"""GPU tests of the drop-in Python API (lz4.block / lz4.frame) against the
+reference's documented behaviour, the golden vectors and the oracle.
+
+Mirrors the reference test strategy: parametrized
+round trips, known-answer vectors, exact exception types and messages,
+corruption and truncation.  All calls run the HIP kernels.
+"""
+import json
+import os
+import struct
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+import lz4  # noqa: E402
+import lz4.block  # noqa: E402
+import lz4.frame  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def golden():
+    with open(os.path.join(GOLDEN, "manifest.json")) as f:
+        man = json.load(f)
+    arr = np.load(os.path.join(GOLDEN, "golden.npz"), allow_pickle=False)
+    return man, arr
+
+
+def _b(arr, key):
+    return arr[key].tobytes()
+
+
+DATA = [b"", os.urandom(8 * 1024), b"0" * 8 * 1024, bytearray(b""), bytearray(os.urandom(8 * 1024)),
+        memoryview(os.urandom(8 * 1024)), b"abc" * 5000]
+
+
+# ------------------------------------------------------------------ block API
+@pytest.mark.parametrize("data", DATA, ids=[f"d{i}" for i in range(len(DATA))])
+@pytest.mark.parametrize("mode", [("default", 1), ("fast", 1), ("fast", 4), ("fast", 0)])
+@pytest.mark.parametrize("store_size", [True, False])
+def test_block_roundtrip(gpu, data, mode, store_size):
+    c = lz4.block.compress(data, mode=mode[0], acceleration=mode[1], store_size=store_size)
+    if store_size:
+        d = lz4.block.decompress(c)
+    else:
+        d = lz4.block.decompress(c, uncompressed_size=len(data))
+    assert d == bytes(data)
+
+
+def test_block_compress_is_reference_bytes(gpu, golden):
+    """lz4.block.compress output == the reference lz4.block.compress output."""
+    man, arr = golden
+    inputs = {e["name"]: _b(arr, e["key"]) for e in man["inputs"]}
+    for e in man["compress"]:
+        if e["mode"] != "block_api":
+            continue
+        data = inputs[e["input"]]
+        mode = "default" if e["accel"] == 1 else "fast"
+        got = lz4.block.compress(data, mode=mode, acceleration=e["accel"], store_size=False)
+        assert got == _b(arr, e["key"]), e["input"]
+
+
+def test_block_decompress_golden_status(gpu, golden):
+    man, arr = golden
+    entries = man["decompress"]
+    res = lz4.block.decompress_many([_b(arr, e["key"]) for e in entries],
+                                    uncompressed_size=[e["cap"] for e in entries], raise_errors=False)
+    for e, r in zip(entries, res):
+        if e["status"] < 0:
+            assert isinstance(r, lz4.block.LZ4BlockError), e
+            assert str(r).endswith(f"Error code: {-e['status']}")
+        else:
+            assert len(r) == e["status"]
+
+
+def test_block_kat(gpu, golden):
+    man, arr = golden
+    for e in man["kat"]:
+        assert lz4.block.decompress(_b(arr, e["key"])) == _b(arr, e["plain"])
+
+
+def test_block_errors(gpu):
+    data = lz4.block.compress(b"A" * 64)
+    with pytest.raises(OverflowError):
+        lz4.block.decompress(data[4:], uncompressed_size=((1 << 32) + 64))
+    with pytest.raises(lz4.block.LZ4BlockError,
+                       match=r"^Decompressor wrote 64 bytes, but 79 bytes expected from header$"):
+        lz4.block.decompress(b"\x4f" + data[1:])
+    msg = r"^Decompression failed: corrupt input or insufficient space in destination buffer. Error code: \d+$"
+    d2 = lz4.block.compress(b"A" * 64, store_size=False)
+    with pytest.raises(lz4.block.LZ4BlockError, match=msg):
+        lz4.block.decompress(d2[4:], uncompressed_size=64)
+    with pytest.raises(lz4.block.LZ4BlockError, match=msg):
+        lz4.block.decompress(d2, uncompressed_size=60)
+    comp = lz4.block.compress(b"A" * 64)
+    for bad in (comp + b"A", comp + comp, comp + comp[4:]):
+        with pytest.raises(lz4.block.LZ4BlockError, match=msg):
+            lz4.block.decompress(bad)
+    inp = b"2099023098234882923049823094823094898239230982349081231290381209380981203981209381238901283098908123109238098123" * 24
+    c = lz4.block.compress(inp)
+    for n in [0, 1]:
+        with pytest.raises(ValueError, match="Input source data size too small"):
+            lz4.block.decompress(c[:n])
+    for n in [24, 25, -2, 27, 67, 85]:
+        with pytest.raises(lz4.block.LZ4BlockError):
+            lz4.block.decompress(c[:n])
+    with pytest.raises(ValueError, match=r"^Invalid size: 0x"):
+        lz4.block.decompress(b"\xff\xff\xff\xff\x00")
+
+
+def test_block_return_bytearray(gpu):
+    data = os.urandom(128 * 1024)
+    c = lz4.block.compress(data)
+    b = lz4.block.compress(data, return_bytearray=True)
+    assert isinstance(b, bytearray) and bytes(b) == c
+    d = lz4.block.decompress(c, return_bytearray=True)
+    assert isinstance(d, bytearray) and bytes(d) == data
+
+
+def test_block_capacity_semantics(gpu):
+    x = b"hello world " * 9   # 108 bytes
+    c = lz4.block.compress(x, store_size=False)
+    assert lz4.block.decompress(c, uncompressed_size=len(x)) == x
+    assert lz4.block.decompress(c, uncompressed_size=len(x) + 1) == x
+    assert lz4.block.decompress(c, uncompressed_size=1000) == x
+    with pytest.raises(lz4.block.LZ4BlockError):
+        lz4.block.decompress(c, uncompressed_size=len(x) - 1)
+
+
+def test_block_dict_decompress(gpu, reference):
+    """dict= decompression matches the reference decoder on blocks that were
+    compressed against a dictionary by the reference (_block.c:101-104)."""
+    import ctypes as C
+    lib = reference.lib
+    lib.LZ4_loadDict.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+    from lz4 import _synth
+    blk = _synth.blocks(3, "text", seed=5)
+    d, x = blk[0].tobytes()[:20000], blk[1].tobytes()[:30000]
+    state = C.create_string_buffer(int(lib.LZ4_sizeofState()))
+    lib.LZ4_resetStream(state)
+    lib.LZ4_loadDict(state, d, len(d))
+    dst = C.create_string_buffer(70000)
+    n = lib.LZ4_compress_fast_continue(state, x, dst, len(x), 70000, 1)
+    comp = dst.raw[:n]
+    assert lz4.block.decompress(comp, uncompressed_size=len(x), dict=d) == x
+    st, _ = reference.decompress(comp, len(x))
+    with pytest.raises(lz4.block.LZ4BlockError, match=f"Error code: {-st}$"):
+        lz4.block.decompress(comp, uncompressed_size=len(x))
+
+
+def test_many_matches_single(gpu):
+    from lz4 import _synth
+    blocks = [b.tobytes() for b in _synth.blocks(32, "silesia", seed=1)]
+    many = lz4.block.compress_many(blocks)
+    assert many == [lz4.block.compress(b) for b in blocks[:4]] + many[4:]
+    assert lz4.block.decompress_many(many) == blocks
+
+
+def test_library_version(gpu):
+    assert lz4.library_version_number() == 10904
+    assert lz4.library_version_string() == "1.9.4"
+
+
+# ------------------------------------------------------------------ frame API
+FRAME_DATA = [b"", os.urandom(8 * 1024), b"0" * 8 * 1024, bytearray(os.urandom(128 * 1024)),
+              os.urandom(512 * 1024), memoryview(b"xyz" * 200000)]
+
+
+@pytest.mark.parametrize("data", FRAME_DATA, ids=[f"f{i}" for i in range(len(FRAME_DATA))])
+@pytest.mark.parametrize("block_size", [4, 5, 6, 7])
+@pytest.mark.parametrize("block_linked", [True, False])
+@pytest.mark.parametrize("checksums", [(False, False), (True, False), (True, True), (False, True)])
+@pytest.mark.parametrize("store_size", [True, False])
+def test_frame_roundtrip(gpu, data, block_size, block_linked, checksums, store_size):
+    cc, bc = checksums
+    c = lz4.frame.compress(data, block_size=block_size, block_linked=block_linked, content_checksum=cc,
+                           block_checksum=bc, store_size=store_size)
+    info = lz4.frame.get_frame_info(c)
+    assert info["content_checksum"] == cc and info["block_checksum"] == bc
+    assert info["skippable"] is False
+    assert info["content_size"] == (len(data) if store_size else 0)
+    if len(data) > info["block_size"]:
+        assert info["block_linked"] == block_linked
+        assert info["block_size_id"] == block_size
+    d, nread = lz4.frame.decompress(c, return_bytes_read=True)
+    assert d == bytes(data) and nread == len(c)
+
+
+def test_frame_independent_is_reference_bytes(gpu, golden, reference):
+    """Independent-block frames are byte-identical to LZ4F_compressFrame."""
+    man, arr = golden
+    inputs = {e["name"]: _b(arr, e["key"]) for e in man["inputs"]}
+    for e in man["frames"]:
+        o = e["opts"]
+        if o.get("linked"):
+            continue
+        data = inputs[e["input"]]
+        got = lz4.frame.compress(data, block_size=o["block_size_id"], block_linked=False,
+                                 content_checksum=o.get("content_checksum", True),
+                                 block_checksum=o.get("block_checksum", False),
+                                 store_size=o.get("store_size", True), compression_level=o.get("level", 0))
+        assert got == _b(arr, e["key"]), o
+
+
+def test_frame_decodes_reference_frames(gpu, golden):
+    man, arr = golden
+    inputs = {e["name"]: _b(arr, e["key"]) for e in man["inputs"]}
+    for e in man["frames"]:
+        assert lz4.frame.decompress(_b(arr, e["key"])) == inputs[e["input"]], e["opts"]
+
+
+def test_reference_decodes_our_frames(gpu, reference):
+    import oracle as O
+    from lz4 import _synth
+    data = _synth.blocks(20, "silesia", seed=8).tobytes()[:1_100_000]
+    for bs in (4, 6, 7):
+        for linked in (True, False):
+            c = lz4.frame.compress(data, block_size=bs, block_linked=linked, content_checksum=True,
+                                   block_checksum=True)
+            code, out = O.ref_decompress_frame(reference, c)
+            assert code == 0 and out == data
+
+
+def test_frame_truncated(gpu):
+    data = os.urandom(256 * 1024)
+    c = lz4.frame.compress(data)
+    with pytest.raises(RuntimeError, match=r"^LZ4F_getFrameInfo failed with code: ERROR_frameHeader_incomplete"):
+        lz4.frame.decompress(c[:6])
+    for i in range(16, len(c) - 1, 4099):
+        with pytest.raises(RuntimeError, match=r"^Frame incomplete. LZ4F_decompress returned:"):
+            lz4.frame.decompress(c[:i])
+
+
+def test_frame_checksum_failures(gpu):
+    data = os.urandom(256 * 1024)
+    c = lz4.frame.compress(data, content_checksum=True)
+    last = struct.unpack("B", c[-1:])[0]
+    with pytest.raises(RuntimeError, match=r"^LZ4F_decompress failed with code: ERROR_contentChecksum_invalid$"):
+        lz4.frame.decompress(c[:-1] + struct.pack("B", last ^ 0x42))
+    c = lz4.frame.compress(data, content_checksum=True, block_checksum=True, return_bytearray=True)
+    c[22] ^= 0x42
+    with pytest.raises(RuntimeError, match=r"^LZ4F_decompress failed with code: ERROR_blockChecksum_invalid$"):
+        lz4.frame.decompress(c)
+
+
+def test_frame_bad_headers(gpu):
+    c = bytearray(lz4.frame.compress(b"hello" * 100))
+    bad = bytearray(c)
+    bad[0] ^= 1
+    with pytest.raises(RuntimeError, match="ERROR_frameType_unknown"):
+        lz4.frame.decompress(bad)
+    bad = bytearray(c)
+    bad[-5 - 4 - 1] ^= 0xFF   # payload byte -> decode fails or checksum
+    bad = bytearray(c)
+    bad[6 + 8] ^= 0xFF        # header checksum byte
+    with pytest.raises(RuntimeError, match="ERROR_headerChecksum_invalid"):
+        lz4.frame.decompress(bad)
+
+
+def test_frame_levels(gpu):
+    data = b"".join(os.urandom(16) * 50 for _ in range(200))
+    for level in (0, 1, 2, -1, -5):
+        assert lz4.frame.decompress(lz4.frame.compress(data, compression_level=level)) == data
+    with pytest.raises(NotImplementedError):
+        lz4.frame.compress(data, compression_level=3)
+
+
+def test_frame_trailing_data_and_multiframe(gpu):
+    a, b = os.urandom(1000), b"q" * 70000
+    ca, cb = lz4.frame.compress(a), lz4.frame.compress(b)
+    d, n = lz4.frame.decompress(ca + cb, return_bytes_read=True)
+    assert d == a and n == len(ca)
+    assert lz4.frame.decompress((ca + cb)[n:]) == b

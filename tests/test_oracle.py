@@ -1,0 +1,158 @@
+"""CPU tests: the oracle (oracle/lz4_oracle.c) against the golden vectors
+generated from the reference lz4libs (tests/golden/make_golden.py), plus a
+differential fuzz against the reference build when it is present."""
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+
+@pytest.fixture(scope="module")
+def golden():
+    with open(os.path.join(GOLDEN, "manifest.json")) as f:
+        man = json.load(f)
+    arr = np.load(os.path.join(GOLDEN, "golden.npz"), allow_pickle=False)
+    return man, arr
+
+
+def _b(arr, key):
+    return arr[key].tobytes()
+
+
+def test_golden_is_v194(golden):
+    man, _ = golden
+    assert man["version"] == 10904
+
+
+def test_compress_matches_golden(oracle, golden):
+    man, arr = golden
+    inputs = {e["name"]: _b(arr, e["key"]) for e in man["inputs"]}
+    n = 0
+    for e in man["compress"]:
+        data = inputs[e["input"]]
+        if e["mode"] == "default":
+            got = oracle.compress(data)
+        else:
+            got = oracle.compress(data, 1, accel=e["accel"])
+        assert got == _b(arr, e["key"]), (e["input"], e["mode"], e["accel"])
+        n += 1
+    assert n > 80
+
+
+def test_decompress_status_matches_golden(oracle, golden):
+    man, arr = golden
+    for e in man["decompress"]:
+        st, _ = oracle.decompress(_b(arr, e["key"]), e["cap"])
+        assert st == e["status"], (e["key"], e["cap"])
+
+
+def test_decompress_roundtrip_golden(oracle, golden):
+    man, arr = golden
+    inputs = {e["name"]: _b(arr, e["key"]) for e in man["inputs"]}
+    for e in man["compress"]:
+        data = inputs[e["input"]]
+        st, out = oracle.decompress(_b(arr, e["key"]), len(data))
+        assert st == len(data) and out == data
+
+
+def test_kat(oracle, golden):
+    man, arr = golden
+    for e in man["kat"]:
+        comp = _b(arr, e["key"])
+        st, out = oracle.decompress(comp[4:], int.from_bytes(comp[:4], "little"))
+        assert st == e["status"]
+        assert out == _b(arr, e["plain"])
+
+
+def test_xxh32_golden(oracle, golden):
+    man, arr = golden
+    inputs = {e["name"]: _b(arr, e["key"]) for e in man["inputs"]}
+    rng = random.Random(4)
+    for e in man["xxh32"]:
+        data = inputs[e["input"]]
+        assert oracle.xxh32(data, e["seed"]) == e["value"]
+        # streaming in random chunks equals one-shot (xxhash.c:451-554)
+        cuts = sorted(rng.randrange(len(data) + 1) for _ in range(3))
+        chunks = [data[a:b] for a, b in zip([0] + cuts, cuts + [len(data)])]
+        assert oracle.xxh32_stream(chunks, e["seed"]) == e["value"]
+
+
+def test_xxh32_vs_pip_xxhash(oracle):
+    xxhash = pytest.importorskip("xxhash")
+    rng = np.random.default_rng(1)
+    for n in list(range(0, 70)) + [1000, 4096, 65537]:
+        d = rng.integers(0, 256, size=n, dtype=np.uint8).tobytes()
+        assert oracle.xxh32(d) == xxhash.xxh32_intdigest(d)
+
+
+def test_frame_fixtures_decode_with_oracle(oracle, golden):
+    """The reference frames' block records parse with the host scanner of
+    lz4.frame and every block decodes (oracle) to the original input."""
+    import struct
+    from lz4.frame._frame import _BLOCK_SIZES, _scan_blocks
+    man, arr = golden
+    inputs = {e["name"]: _b(arr, e["key"]) for e in man["inputs"]}
+    for e in man["frames"]:
+        fr = memoryview(_b(arr, e["key"]))
+        flg, bd = fr[4], fr[5]
+        hsize = 7 + (8 if flg & 8 else 0) + (4 if flg & 1 else 0)
+        info = {"block_checksum": bool(flg & 0x10), "content_checksum": bool(flg & 4),
+                "block_size": _BLOCK_SIZES[(bd >> 4) & 7], "block_linked": not (flg & 0x20)}
+        recs, state = _scan_blocks(fr, hsize, info)
+        assert state[0] == "end" and state[1] == len(fr)
+        out = b""
+        for raw, pos, size, crc in recs:
+            blk = bytes(fr[pos:pos + size])
+            if raw:
+                out += blk
+            elif info["block_linked"]:
+                st, dec = oracle.decompress(blk, info["block_size"], dict_=out[-65536:] if out else None)
+                assert st >= 0
+                out += dec
+            else:
+                st, dec = oracle.decompress(blk, info["block_size"])
+                assert st >= 0
+                out += dec
+            if crc >= 0:
+                assert struct.unpack_from("<I", fr, crc)[0] == oracle.xxh32(blk)
+        assert out == inputs[e["input"]]
+        if info["content_checksum"]:
+            assert struct.unpack_from("<I", fr, len(fr) - 4)[0] == oracle.xxh32(out)
+
+
+def test_optimal_bsid():
+    from lz4.frame._frame import _optimal_bsid
+    assert _optimal_bsid(0, 10) == 0
+    assert _optimal_bsid(7, 10) == 4
+    assert _optimal_bsid(7, 65537) == 5
+    assert _optimal_bsid(7, 300000) == 6
+    assert _optimal_bsid(7, 5 << 20) == 7
+    assert _optimal_bsid(4, 5 << 20) == 4
+
+
+def test_differential_vs_reference(oracle, reference):
+    """Oracle vs the reference build on fresh random cases (this container)."""
+    from lz4 import _synth
+    rng = random.Random(99)
+    blocks = _synth.blocks(16, "silesia", seed=123)
+    for i in range(300):
+        b = blocks[rng.randrange(16)].tobytes()
+        n = rng.choice([0, 3, 13, 50, 700, 5000, 65536])
+        o = rng.randrange(0, 65536 - n + 1)
+        x = b[o:o + n]
+        assert oracle.compress(x) == reference.compress_default(x)
+        acc = rng.choice([1, 1, 3, 50])
+        assert oracle.compress(x, 1, accel=acc) == reference.compress_block_api(x, acc)
+        c = bytearray(reference.compress_default(x))
+        for _ in range(rng.randrange(3)):
+            if c:
+                c[rng.randrange(len(c))] = rng.randrange(256)
+        cap = rng.choice([n, n + 5, max(0, n - 2)])
+        assert oracle.decompress(bytes(c), cap) == reference.decompress(bytes(c), cap)
+        d = b[:rng.randrange(1, 70000)]
+        if c:
+            assert oracle.decompress(bytes(c), cap, dict_=d) == reference.decompress(bytes(c), cap, dict_=d)
