@@ -37,10 +37,14 @@ __device__ __forceinline__ uint32_t ld16le(const uint8_t* p) {
 // touches memory past p + avail).
 __device__ __forceinline__ u32x4 ld16_guarded(const uint8_t* p, int64_t avail) {
     if (avail >= 16) return ld16(p);
-    uint32_t w[4] = {0, 0, 0, 0};
-    for (int k = 0; k < 16; ++k)
-        if (k < avail) w[k >> 2] |= (uint32_t)p[k] << ((k & 3) * 8);
-    return u32x4{w[0], w[1], w[2], w[3]};
+    uint64_t lo = 0, hi = 0;
+    const int n = avail <= 0 ? 0 : (int)avail;
+    for (int k = 0; k < n; ++k) {
+        const uint64_t b = p[k];
+        if (k < 8) lo |= b << (8 * k);
+        else hi |= b << (8 * (k - 8));
+    }
+    return u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
 }
 
 // The 4 bytes starting at byte k (0..15) of the 16-byte window w; bytes past

@@ -23,6 +23,9 @@
 #include "lz4m_common.h"
 #include "../../include/lz4m.h"
 
+#include <stdlib.h>
+#include <string.h>
+
 namespace lz4m {
 
 constexpr int64_t kCoopMin = 64;   // copies longer than this go wave-cooperative
@@ -44,7 +47,148 @@ struct Lane {
     int64_t ip, op;
     int32_t result;
     bool fast, live;
+    // RING mode: the lane's 128-byte LDS output ring holds output bytes
+    // [F - 64, op); [0, F) is already in global memory (F % 64 == 0).
+    uint8_t* ring;
+    int64_t F;
 };
+
+// ---------------------------------------------------------- LDS output ring
+// Output is assembled in a per-lane LDS ring and leaves for HBM in whole,
+// contiguous 64-byte chunks (4 x 16-byte stores by one lane), so every HBM
+// line is written once instead of piecemeal by 1-16 byte stores from
+// thousands of interleaved lane streams.  Match sources within the ring's
+// window come from LDS; older ones from the block's flushed output.
+constexpr int64_t kRing = 128;
+
+// bytes [sh, sh + 16) of the 32-byte value a || b (sh 0..15)
+__device__ __forceinline__ u32x4 funnel16(u32x4 a, u32x4 b, uint32_t sh) {
+    const uint32_t q = sh >> 2, r = sh & 3;
+    const uint32_t d0 = q == 0 ? a.x : q == 1 ? a.y : q == 2 ? a.z : a.w;
+    const uint32_t d1 = q == 0 ? a.y : q == 1 ? a.z : q == 2 ? a.w : b.x;
+    const uint32_t d2 = q == 0 ? a.z : q == 1 ? a.w : q == 2 ? b.x : b.y;
+    const uint32_t d3 = q == 0 ? a.w : q == 1 ? b.x : q == 2 ? b.y : b.z;
+    const uint32_t d4 = q == 0 ? b.x : q == 1 ? b.y : q == 2 ? b.z : b.w;
+    return u32x4{__builtin_amdgcn_alignbyte(d1, d0, r), __builtin_amdgcn_alignbyte(d2, d1, r),
+                 __builtin_amdgcn_alignbyte(d3, d2, r), __builtin_amdgcn_alignbyte(d4, d3, r)};
+}
+
+__device__ __forceinline__ u32x4 ring_read16(const uint8_t* ring, int64_t pos) {
+    const uint32_t r = (uint32_t)pos & (uint32_t)(kRing - 1);
+    if (r <= kRing - 16) return ld16(ring + r);   // unaligned ds_read_b128
+    const uint32_t a0 = r & ~15u;
+    return funnel16(ld16(ring + a0), ld16(ring), r & 15u);
+}
+
+// Store exactly k (0..16) bytes of v at p (LDS or global, any alignment).
+__device__ __forceinline__ void put_exact(uint8_t* p, u32x4 v, uint32_t k) {
+    if (k == 16) {
+        st16(p, v);
+        return;
+    }
+    uint32_t o = 0;
+    if (k & 8) {
+        const uint64_t x = ((uint64_t)v.y << 32) | v.x;
+        __builtin_memcpy(p, &x, 8);
+        o = 8;
+    }
+    if (k & 4) {
+        const uint32_t x = window_dword(v, o);
+        __builtin_memcpy(p + o, &x, 4);
+        o += 4;
+    }
+    if (k & 2) {
+        const uint16_t x = (uint16_t)window_dword(v, o);
+        __builtin_memcpy(p + o, &x, 2);
+        o += 2;
+    }
+    if (k & 1) p[o] = (uint8_t)window_dword(v, o);
+}
+
+__device__ __forceinline__ void ring_write(uint8_t* ring, int64_t pos, u32x4 v, uint32_t k) {
+    const uint32_t r = (uint32_t)pos & (uint32_t)(kRing - 1);
+    const uint32_t n1 = k < (uint32_t)kRing - r ? k : (uint32_t)kRing - r;
+    put_exact(ring + r, v, n1);
+    if (k > n1) put_exact(ring, funnel16(v, u32x4{0, 0, 0, 0}, n1), k - n1);
+}
+
+__device__ __forceinline__ void ring_flush(Lane& L) {   // chunk [F, F + 64) is complete
+    const uint8_t* r = L.ring + (L.F & (kRing - 1));
+    uint8_t* d = L.dst + L.F;
+    const u32x4 a = ld16(r), b = ld16(r + 16), c = ld16(r + 32), e = ld16(r + 48);
+    st16(d, a);
+    st16(d + 16, b);
+    st16(d + 32, c);
+    st16(d + 48, e);
+    L.F += 64;
+}
+
+// Before writing at output position p (p < F + 128): keep p < F + 64, so the
+// ring still holds [F - 64, p) while the piece is produced.
+__device__ __forceinline__ void ring_sync(Lane& L, int64_t p) {
+    if (p >= L.F + 64) ring_flush(L);
+}
+
+// 16 output bytes from q as a match source: ring if q >= F - 64, else the
+// flushed output (q + 16 <= F there).
+__device__ __forceinline__ u32x4 out_read16(const Lane& L, int64_t q) {
+    return q >= L.F - 64 ? ring_read16(L.ring, q) : ld16(L.dst + q);
+}
+
+__device__ __forceinline__ void ring_literal(Lane& L, int64_t op, int64_t ip, int64_t len) {
+    for (int64_t i = 0; i < len; i += 16) {
+        const int64_t p = op + i;
+        ring_sync(L, p);
+        const u32x4 v = ld16_guarded(L.src + ip + i, L.iend - ip - i);
+        ring_write(L.ring, p, v, (uint32_t)(len - i < 16 ? len - i : 16));
+    }
+}
+
+__device__ __forceinline__ void ring_match(Lane& L, int64_t op, int64_t off, int64_t len) {
+    if (off >= 16) {
+        for (int64_t i = 0; i < len; i += 16) {
+            const int64_t p = op + i;
+            ring_sync(L, p);
+            const u32x4 v = out_read16(L, p - off);
+            ring_write(L.ring, p, v, (uint32_t)(len - i < 16 ? len - i : 16));
+        }
+        return;
+    }
+    u32x4 pat;
+    int64_t step;
+    if (off == 0) {   // lz4.c:2300-2307
+        pat = u32x4{0, 0, 0, 0};
+        step = 16;
+    } else {
+        ring_sync(L, op);
+        pat = period_pattern(out_read16(L, op - off), (uint32_t)off);
+        step = 16 - (16 % off);
+    }
+    for (int64_t i = 0; i < len;) {
+        const int64_t p = op + i;
+        ring_sync(L, p);
+        const int64_t k = len - i <= 16 ? len - i : step;
+        ring_write(L.ring, p, pat, (uint32_t)k);
+        i += k;
+    }
+}
+
+// Block done (or failed): flush [F, end) exactly.
+__device__ __forceinline__ void ring_finish(Lane& L, int64_t end) {
+    while (L.F + 64 <= end) ring_flush(L);
+    for (int64_t p = L.F; p < end; p += 16) {
+        const int64_t k = end - p < 16 ? end - p : 16;
+        put_exact(L.dst + p, ring_read16(L.ring, p), (uint32_t)k);
+    }
+}
+
+// After a wave-cooperative copy wrote [.., E) straight to HBM: restart the
+// ring at F = E rounded down to 64, reloading [F - 64, E).
+__device__ __forceinline__ void ring_reload(Lane& L, int64_t E) {
+    L.F = E & ~(int64_t)63;
+    const int64_t b = L.F >= 64 ? L.F - 64 : 0;
+    for (int64_t x = b; x < E; x += 16) st16(L.ring + (x & (kRing - 1)), ld16_guarded(L.dst + x, L.oend - x));
+}
 
 // ---------------------------------------------------------------- lane copies
 // Non-overlapping copy by the owning lane.  Reads never pass s_room, writes
@@ -169,21 +313,39 @@ __device__ __forceinline__ bool read_len(const uint8_t* src, int64_t& ip, int64_
     return true;
 }
 
+template <bool RING>
 __device__ __forceinline__ void emit_literal(Lane& L, int64_t ip, int64_t op, int64_t lit, Copy& c,
                                              bool deferred) {
     if (lit == 0) return;
     if (deferred || lit > kCoopMin) {
         c = Copy{kLiteral, op, ip, lit};
+    } else if (RING) {
+        ring_literal(L, op, ip, lit);
     } else {
         lane_copy(L.dst + op, L.src + ip, lit, L.oend - op, L.iend - ip);
     }
 }
 
+template <bool RING>
 __device__ __forceinline__ void emit_match(Lane& L, int64_t op, int64_t off, int64_t ml, Copy& c, bool deferred) {
     if (deferred || ml > kCoopMin) {
         c = Copy{kMatch, op, off, ml};
+    } else if (RING) {
+        ring_match(L, op, off, ml);
     } else {
         lane_match(L.dst + op, off, ml, L.oend - op);
+    }
+}
+
+// Literal bytes 1..lit (lit <= 14) of the token window.
+template <bool RING>
+__device__ __forceinline__ void window_literal(Lane& L, int64_t op, u32x4 w, int64_t lit) {
+    if (RING) {
+        if (lit == 0) return;
+        ring_sync(L, op);
+        ring_write(L.ring, op, window_shift1(w), (uint32_t)lit);
+    } else {
+        st16(L.dst + op, window_shift1(w));   // wild 16-byte store, inside the oend-32 margin
     }
 }
 
@@ -205,8 +367,8 @@ __device__ __noinline__ void dict_match(Lane& L, int64_t op, int64_t off, int64_
 }
 
 // One sequence of block L.  Deferred copies land in lc / mc.
-template <bool DICT>
-__device__ void decode_step(Lane& L, Copy& lc, Copy& mc) {
+template <bool DICT, bool RING>
+__device__ __forceinline__ void decode_step(Lane& L, Copy& lc, Copy& mc) {
     const u32x4 w = ld16_guarded(L.src + L.ip, L.iend - L.ip);
     const uint32_t tok = w.x & 0xFFu;
     int64_t ip = L.ip + 1;
@@ -226,7 +388,7 @@ __device__ void decode_step(Lane& L, Copy& lc, Copy& mc) {
                 L.fast = false;
                 goto literal_tail;
             }
-            emit_literal(L, ip, op, lit, lc, false);
+            emit_literal<RING>(L, ip, op, lit, lc, false);
             deferred = lc.kind != kNone;
             ip += lit;
             op += lit;
@@ -236,8 +398,8 @@ __device__ void decode_step(Lane& L, Copy& lc, Copy& mc) {
                 L.fast = false;
                 goto literal_tail;
             }
-            // literals are bytes 1..lit of the token window (wild 16-byte store)
-            st16(L.dst + op, window_shift1(w));
+            // literals are bytes 1..lit of the token window
+            window_literal<RING>(L, op, w, lit);
             off = lit <= 13 ? (window_dword(w, (uint32_t)(1 + lit)) & 0xFFFFu) : ld16le(L.src + ip + lit);
             ip += lit;
             op += lit;
@@ -259,7 +421,7 @@ __device__ void decode_step(Lane& L, Copy& lc, Copy& mc) {
                 goto match_tail;
             }
             if (off >= 8 && off <= op) {
-                emit_match(L, op, off, ml, mc, deferred);
+                emit_match<RING>(L, op, off, ml, mc, deferred);
                 op += ml;
                 goto done;
             }
@@ -272,20 +434,24 @@ __device__ void decode_step(Lane& L, Copy& lc, Copy& mc) {
             op += ml;
             goto done;
         }
-        emit_match(L, op, off, ml, mc, deferred);
+        emit_match<RING>(L, op, off, ml, mc, deferred);
         op += ml;
         goto done;
     }
 
     // safe phase, lz4.c:2114-2329
     if (lit != 15 && ip < iend - 16 && op <= oend - 32) {   // shortcut, lz4.c:2128-2158
-        st16(L.dst + op, window_shift1(w));
+        window_literal<RING>(L, op, w, lit);
         off = lit <= 13 ? (window_dword(w, (uint32_t)(1 + lit)) & 0xFFFFu) : ld16le(L.src + ip + lit);
         op += lit;
         ip += lit + 2;
         ml = tok & 15;
         if (ml != 15 && off >= 8 && off <= op) {
-            lane_match(L.dst + op, off, ml + 4, oend - op);
+            if (RING) {
+                ring_match(L, op, off, ml + 4);
+            } else {
+                lane_match(L.dst + op, off, ml + 4, oend - op);
+            }
             op += ml + 4;
             goto done;
         }
@@ -298,14 +464,14 @@ __device__ void decode_step(Lane& L, Copy& lc, Copy& mc) {
 literal_tail:   // lz4.c:2172-2229
     if (op + lit > oend - 12 || ip + lit > iend - 8) {
         if (ip + lit != iend || op + lit > oend) goto fail;
-        emit_literal(L, ip, op, lit, lc, false);   // last literals: exact (never past oend / iend)
+        emit_literal<RING>(L, ip, op, lit, lc, false);   // last literals: exact (never past oend / iend)
         op += lit;
         L.result = (int32_t)op;
         L.live = false;
         L.op = op;
         return;
     }
-    emit_literal(L, ip, op, lit, lc, false);
+    emit_literal<RING>(L, ip, op, lit, lc, false);
     deferred = lc.kind != kNone;
     ip += lit;
     op += lit;
@@ -328,7 +494,7 @@ match_tail:   // lz4.c:2248-2328
         goto done;
     }
     if (op + ml > oend - 5) goto fail;
-    emit_match(L, op, off, ml, mc, deferred);
+    emit_match<RING>(L, op, off, ml, mc, deferred);
     op += ml;
 done:
     L.ip = ip;
@@ -389,7 +555,7 @@ __global__ __launch_bounds__(256) void decompress_kernel(const uint8_t* __restri
 
     while (__any(L.live)) {
         Copy lc{kNone, 0, 0, 0}, mc{kNone, 0, 0, 0};
-        if (L.live) decode_step<DICT>(L, lc, mc);
+        if (L.live) decode_step<DICT, false>(L, lc, mc);
         uint64_t pend = __ballot(lc.kind != kNone || mc.kind != kNone);
         if (pend == 0) continue;
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // lane stores visible to the wave
@@ -421,6 +587,105 @@ __global__ __launch_bounds__(256) void decompress_kernel(const uint8_t* __restri
     if (i < n) status[i] = L.result;
 }
 
+
+// One round of wave-cooperative long copies in RING mode.  Each lane with a
+// copy [dpos, E) first writes the head up to the next 64-byte boundary A
+// through its ring and flushes, so [0, A) is in HBM; the wave then copies
+// [A, E) of every such lane straight to HBM at wave width (lane order); the
+// lane finally restarts its ring from HBM at E.
+__device__ __forceinline__ void ring_coop(Lane& L, const Copy& c, uint32_t lane) {
+    int64_t A = 0, E = 0;
+    bool coop = false;
+    if (c.kind != kNone) {
+        E = c.dpos + c.len;
+        const int64_t up = (c.dpos + 63) & ~(int64_t)63;
+        A = up < E ? up : E;
+        if (A > c.dpos) {
+            if (c.kind == kLiteral) {
+                ring_literal(L, c.dpos, c.arg, A - c.dpos);
+            } else {
+                ring_match(L, c.dpos, c.arg, A - c.dpos);
+            }
+        }
+        if (A < E) {
+            while (L.F + 64 <= A) ring_flush(L);
+            coop = true;
+        }
+    }
+    uint64_t pend = __ballot(coop);
+    if (pend == 0) return;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // flushed heads visible to the wave
+    while (pend) {
+        const int l = __builtin_ctzll(pend);
+        pend &= pend - 1;
+        uint8_t* d = readlane_ptr(L.dst, l);
+        const int64_t oend = readlane64(L.oend, l);
+        const int64_t a = readlane64(A, l), e = readlane64(E, l);
+        if (__builtin_amdgcn_readlane(c.kind, l) == kLiteral) {
+            const uint8_t* s = readlane_ptr(L.src, l);
+            const int64_t iend = readlane64(L.iend, l);
+            const int64_t sp = readlane64(c.arg, l) + (a - readlane64(c.dpos, l));
+            wave_literal(d + a, s + sp, e - a, oend - a, iend - sp, lane);
+        } else {
+            wave_match(d + a, readlane64(c.arg, l), e - a, oend - a, lane);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    }
+    if (coop) ring_reload(L, E);
+}
+
+// Independent blocks without a dictionary (the hot path).  Same lane-per-
+// block state machine as decompress_kernel, output through the LDS ring.
+__global__ __launch_bounds__(256) void ring_decompress_kernel(const uint8_t* __restrict__ src,
+                                                              const int64_t* __restrict__ src_off,
+                                                              const int32_t* __restrict__ src_len, uint8_t* dst,
+                                                              const int64_t* __restrict__ dst_off,
+                                                              const int32_t* __restrict__ dst_cap,
+                                                              int32_t* __restrict__ status, int64_t n) {
+    __shared__ __attribute__((aligned(16))) uint8_t rings[256 * kRing];
+    const uint32_t lane = lane_id();
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    Lane L;
+    L.live = false;
+    L.result = -1;
+    L.ring = rings + threadIdx.x * kRing;
+    L.F = 0;
+    bool open = false;   // ring holds output not yet in HBM
+    if (i < n) {
+        L.src = src + src_off[i];
+        L.dst = dst + dst_off[i];
+        L.iend = src_len[i];
+        L.oend = dst_cap[i];
+        L.ip = 0;
+        L.op = 0;
+        L.dict_len = 0;
+        L.dict_end = nullptr;
+        if (L.oend < 0) {
+            L.result = -1;   // lz4.c:1950
+        } else if (L.oend == 0) {
+            L.result = (L.iend == 1 && L.src[0] == 0) ? 0 : -1;   // lz4.c:1978-1982
+        } else if (L.iend <= 0) {
+            L.result = -1;   // lz4.c:1983
+        } else {
+            L.fast = L.oend >= 64;
+            L.live = true;
+            open = true;
+        }
+    }
+    while (__any(L.live)) {
+        Copy lc{kNone, 0, 0, 0}, mc{kNone, 0, 0, 0};
+        if (L.live) decode_step<false, true>(L, lc, mc);
+        if (__ballot(lc.kind != kNone || mc.kind != kNone)) {
+            ring_coop(L, lc, lane);   // literal before match
+            ring_coop(L, mc, lane);
+        }
+        if (open && !L.live) {
+            ring_finish(L, L.result >= 0 ? (int64_t)L.result : L.op);
+            open = false;
+        }
+    }
+    if (i < n) status[i] = L.result;
+}
 
 // Linked-block frames (lz4frame.c:1853-1856, LZ4F_updateDict): block i may
 // reference the output of blocks < i, so the chain decodes in order on one
@@ -468,7 +733,7 @@ __global__ __launch_bounds__(64) void decompress_chain_kernel(const uint8_t* __r
         }
         while (__any(L.live)) {
             Copy lc{kNone, 0, 0, 0}, mc{kNone, 0, 0, 0};
-            if (L.live) decode_step<true>(L, lc, mc);
+            if (L.live) decode_step<true, false>(L, lc, mc);
             const uint64_t pend = __ballot(lc.kind != kNone || mc.kind != kNone);
             if (pend == 0) continue;
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
@@ -511,8 +776,18 @@ extern "C" int lz4m_decompress_batch(const uint8_t* d_src, const int64_t* d_src_
     if (n < 0) return LZ4M_EINVAL;
     if (n == 0) return 0;
     const int64_t grid = (n + 255) / 256;
-    hipLaunchKernelGGL(decompress_kernel<false>, dim3((uint32_t)grid), dim3(256), 0, (hipStream_t)stream, d_src,
-                       d_src_off, d_src_len, d_dst, d_dst_off, d_dst_cap, nullptr, nullptr, nullptr, d_status, n);
+    // LZ4M_DECODER=direct selects the ring-less kernel (A/B measurements only)
+    static const bool direct = [] {
+        const char* e = getenv("LZ4M_DECODER");
+        return e != nullptr && strcmp(e, "direct") == 0;
+    }();
+    if (direct) {
+        hipLaunchKernelGGL(decompress_kernel<false>, dim3((uint32_t)grid), dim3(256), 0, (hipStream_t)stream, d_src,
+                           d_src_off, d_src_len, d_dst, d_dst_off, d_dst_cap, nullptr, nullptr, nullptr, d_status, n);
+    } else {
+        hipLaunchKernelGGL(ring_decompress_kernel, dim3((uint32_t)grid), dim3(256), 0, (hipStream_t)stream, d_src,
+                           d_src_off, d_src_len, d_dst, d_dst_off, d_dst_cap, d_status, n);
+    }
     return (int)hipGetLastError();
 }
 
