@@ -64,6 +64,20 @@ int lz4m_decompress_batch(const uint8_t* d_src, const int64_t* d_src_off, const 
                           uint8_t* d_dst, const int64_t* d_dst_off, const int32_t* d_dst_cap,
                           int32_t* d_status, int64_t n, lz4m_stream_t stream);
 
+/* Device scratch lz4m_decompress_batch_ws needs (the block work-queue
+ * counter of the persistent decoder). */
+size_t lz4m_decompress_workspace_bytes(void);
+
+/* lz4m_decompress_batch with caller-provided device scratch of at least
+ * lz4m_decompress_workspace_bytes() bytes, 8-byte aligned, not shared with a
+ * concurrently running call.  lz4m_decompress_batch itself draws its scratch
+ * from a small library-owned pool (1024 slots used round-robin), so use this
+ * form when very many decodes may be in flight at once. */
+int lz4m_decompress_batch_ws(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len,
+                             uint8_t* d_dst, const int64_t* d_dst_off, const int32_t* d_dst_cap,
+                             int32_t* d_status, int64_t n, void* d_work, size_t work_bytes,
+                             lz4m_stream_t stream);
+
 /*
  * Batched LZ4_decompress_safe_usingDict with the dictionary in a separate
  * buffer (usingExtDict, lz4.c:2612-2625, the `dict=` argument of

@@ -26,6 +26,9 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
+#include <mutex>
+
 namespace lz4m {
 
 constexpr int64_t kCoopMin = 64;   // copies longer than this go wave-cooperative
@@ -47,40 +50,61 @@ struct Lane {
     int64_t ip, op;
     int32_t result;
     bool fast, live;
-    // RING mode: the lane's 128-byte LDS output ring holds output bytes
-    // [F - 64, op); [0, F) is already in global memory (F % 64 == 0).
-    uint8_t* ring;
+    // STAGE mode (the hot kernel): an LDS output stage holding output bytes
+    // [F - 16, op) at offset p - F + 16 ([0, F) is in HBM, F % 64 == 0) and
+    // an LDS input window holding compressed bytes [ib, ib + 64).
+    uint8_t* stage;
     int64_t F;
+    uint8_t* win;
+    int64_t ib;
 };
 
-// ---------------------------------------------------------- LDS output ring
-// Output is assembled in a per-lane LDS ring and leaves for HBM in whole,
-// contiguous 64-byte chunks (4 x 16-byte stores by one lane), so every HBM
-// line is written once instead of piecemeal by 1-16 byte stores from
-// thousands of interleaved lane streams.  Match sources within the ring's
-// window come from LDS; older ones from the block's flushed output.
-constexpr int64_t kRing = 128;
+// ------------------------------------------------------ LDS staging (hot kernel)
+// Output is assembled in a per-lane LDS stage and leaves for HBM in whole,
+// contiguous 64-byte chunks (4 x 16-byte stores by one lane): every HBM line
+// is written once, instead of piecemeal by 1-16 byte stores from thousands of
+// interleaved lane streams.  The token stream is read through a per-lane
+// 64-byte window refilled by 16-byte loads of consecutive addresses, so each
+// compressed byte crosses the memory hierarchy about once (reading tokens
+// straight from HBM cost ~3 cache-line fetches per sequence).  Both buffers
+// are linear and rebased as they advance, so every access is one unaligned
+// ds_read/ds_write_b128 without wrap-around logic; stores into the stage are
+// wild 16-byte stores (like the reference's wild copies) and only the final
+// partial chunk is written to HBM byte-exactly.
+constexpr int kStage = 128;
+constexpr int kWin = 64;
 
-// bytes [sh, sh + 16) of the 32-byte value a || b (sh 0..15)
-__device__ __forceinline__ u32x4 funnel16(u32x4 a, u32x4 b, uint32_t sh) {
-    const uint32_t q = sh >> 2, r = sh & 3;
-    const uint32_t d0 = q == 0 ? a.x : q == 1 ? a.y : q == 2 ? a.z : a.w;
-    const uint32_t d1 = q == 0 ? a.y : q == 1 ? a.z : q == 2 ? a.w : b.x;
-    const uint32_t d2 = q == 0 ? a.z : q == 1 ? a.w : q == 2 ? b.x : b.y;
-    const uint32_t d3 = q == 0 ? a.w : q == 1 ? b.x : q == 2 ? b.y : b.z;
-    const uint32_t d4 = q == 0 ? b.x : q == 1 ? b.y : q == 2 ? b.z : b.w;
-    return u32x4{__builtin_amdgcn_alignbyte(d1, d0, r), __builtin_amdgcn_alignbyte(d2, d1, r),
-                 __builtin_amdgcn_alignbyte(d3, d2, r), __builtin_amdgcn_alignbyte(d4, d3, r)};
+__device__ __forceinline__ uint8_t* stage_at(const Lane& L, int64_t p) { return L.stage + (p - L.F + 16); }
+
+// Chunk [F, F + 64) is final: write it to HBM and rebase the stage by 64.
+__device__ __forceinline__ void stage_flush(Lane& L) {
+    const u32x4 a = ld16(L.stage + 16), b = ld16(L.stage + 32), c = ld16(L.stage + 48), d = ld16(L.stage + 64);
+    const u32x4 e = ld16(L.stage + 80), f = ld16(L.stage + 96), g = ld16(L.stage + 112);
+    uint8_t* o = L.dst + L.F;
+    st16(o, a);
+    st16(o + 16, b);
+    st16(o + 32, c);
+    st16(o + 48, d);
+    st16(L.stage, d);
+    st16(L.stage + 16, e);
+    st16(L.stage + 32, f);
+    st16(L.stage + 48, g);
+    L.F += 64;
 }
 
-__device__ __forceinline__ u32x4 ring_read16(const uint8_t* ring, int64_t pos) {
-    const uint32_t r = (uint32_t)pos & (uint32_t)(kRing - 1);
-    if (r <= kRing - 16) return ld16(ring + r);   // unaligned ds_read_b128
-    const uint32_t a0 = r & ~15u;
-    return funnel16(ld16(ring + a0), ld16(ring), r & 15u);
+// Before a 16-byte store at output position p (all bytes below p final):
+// keep p < F + 64, so stores stay inside the stage.
+__device__ __forceinline__ void stage_sync(Lane& L, int64_t p) {
+    if (p >= L.F + 64) stage_flush(L);
 }
 
-// Store exactly k (0..16) bytes of v at p (LDS or global, any alignment).
+// 16 output bytes from q, a match source: the stage if q >= F - 16, else
+// HBM (then q + 16 <= F: already flushed).
+__device__ __forceinline__ u32x4 out_read16(const Lane& L, int64_t q) {
+    return q >= L.F - 16 ? ld16(stage_at(L, q)) : ld16(L.dst + q);
+}
+
+// Store exactly k (0..16) bytes of v at p (any alignment).
 __device__ __forceinline__ void put_exact(uint8_t* p, u32x4 v, uint32_t k) {
     if (k == 16) {
         st16(p, v);
@@ -105,89 +129,84 @@ __device__ __forceinline__ void put_exact(uint8_t* p, u32x4 v, uint32_t k) {
     if (k & 1) p[o] = (uint8_t)window_dword(v, o);
 }
 
-__device__ __forceinline__ void ring_write(uint8_t* ring, int64_t pos, u32x4 v, uint32_t k) {
-    const uint32_t r = (uint32_t)pos & (uint32_t)(kRing - 1);
-    const uint32_t n1 = k < (uint32_t)kRing - r ? k : (uint32_t)kRing - r;
-    put_exact(ring + r, v, n1);
-    if (k > n1) put_exact(ring, funnel16(v, u32x4{0, 0, 0, 0}, n1), k - n1);
-}
-
-__device__ __forceinline__ void ring_flush(Lane& L) {   // chunk [F, F + 64) is complete
-    const uint8_t* r = L.ring + (L.F & (kRing - 1));
-    uint8_t* d = L.dst + L.F;
-    const u32x4 a = ld16(r), b = ld16(r + 16), c = ld16(r + 32), e = ld16(r + 48);
-    st16(d, a);
-    st16(d + 16, b);
-    st16(d + 32, c);
-    st16(d + 48, e);
-    L.F += 64;
-}
-
-// Before writing at output position p (p < F + 128): keep p < F + 64, so the
-// ring still holds [F - 64, p) while the piece is produced.
-__device__ __forceinline__ void ring_sync(Lane& L, int64_t p) {
-    if (p >= L.F + 64) ring_flush(L);
-}
-
-// 16 output bytes from q as a match source: ring if q >= F - 64, else the
-// flushed output (q + 16 <= F there).
-__device__ __forceinline__ u32x4 out_read16(const Lane& L, int64_t q) {
-    return q >= L.F - 64 ? ring_read16(L.ring, q) : ld16(L.dst + q);
-}
-
-__device__ __forceinline__ void ring_literal(Lane& L, int64_t op, int64_t ip, int64_t len) {
+// Literal of len <= 64 bytes read from the compressed block.
+__device__ __forceinline__ void stage_literal(Lane& L, int64_t op, int64_t ip, int64_t len) {
     for (int64_t i = 0; i < len; i += 16) {
-        const int64_t p = op + i;
-        ring_sync(L, p);
-        const u32x4 v = ld16_guarded(L.src + ip + i, L.iend - ip - i);
-        ring_write(L.ring, p, v, (uint32_t)(len - i < 16 ? len - i : 16));
+        stage_sync(L, op + i);
+        st16(stage_at(L, op + i), ld16_guarded(L.src + ip + i, L.iend - ip - i));
     }
 }
 
-__device__ __forceinline__ void ring_match(Lane& L, int64_t op, int64_t off, int64_t len) {
+// Match of len <= 64 bytes (zeros for off == 0, lz4.c:2300-2307).
+__device__ __forceinline__ void stage_match(Lane& L, int64_t op, int64_t off, int64_t len) {
     if (off >= 16) {
         for (int64_t i = 0; i < len; i += 16) {
-            const int64_t p = op + i;
-            ring_sync(L, p);
-            const u32x4 v = out_read16(L, p - off);
-            ring_write(L.ring, p, v, (uint32_t)(len - i < 16 ? len - i : 16));
+            stage_sync(L, op + i);
+            st16(stage_at(L, op + i), out_read16(L, op + i - off));
         }
         return;
     }
     u32x4 pat;
     int64_t step;
-    if (off == 0) {   // lz4.c:2300-2307
+    if (off == 0) {
         pat = u32x4{0, 0, 0, 0};
         step = 16;
     } else {
-        ring_sync(L, op);
-        pat = period_pattern(out_read16(L, op - off), (uint32_t)off);
+        stage_sync(L, op);
+        pat = period_pattern(out_read16(L, op - off), (uint32_t)off);   // op - off >= F - 16
         step = 16 - (16 % off);
     }
-    for (int64_t i = 0; i < len;) {
-        const int64_t p = op + i;
-        ring_sync(L, p);
-        const int64_t k = len - i <= 16 ? len - i : step;
-        ring_write(L.ring, p, pat, (uint32_t)k);
-        i += k;
+    for (int64_t i = 0; i < len; i += step) {
+        stage_sync(L, op + i);
+        st16(stage_at(L, op + i), pat);
     }
 }
 
-// Block done (or failed): flush [F, end) exactly.
-__device__ __forceinline__ void ring_finish(Lane& L, int64_t end) {
-    while (L.F + 64 <= end) ring_flush(L);
+// Block done (or failed): flush [F, end) byte-exactly.
+__device__ __forceinline__ void stage_finish(Lane& L, int64_t end) {
+    while (L.F + 64 <= end) stage_flush(L);
     for (int64_t p = L.F; p < end; p += 16) {
-        const int64_t k = end - p < 16 ? end - p : 16;
-        put_exact(L.dst + p, ring_read16(L.ring, p), (uint32_t)k);
+        put_exact(L.dst + p, ld16(stage_at(L, p)), (uint32_t)(end - p < 16 ? end - p : 16));
     }
 }
 
 // After a wave-cooperative copy wrote [.., E) straight to HBM: restart the
-// ring at F = E rounded down to 64, reloading [F - 64, E).
-__device__ __forceinline__ void ring_reload(Lane& L, int64_t E) {
+// stage at F = E rounded down to 64, reloading [F - 16, E) from HBM.
+__device__ __forceinline__ void stage_reload(Lane& L, int64_t E) {
     L.F = E & ~(int64_t)63;
-    const int64_t b = L.F >= 64 ? L.F - 64 : 0;
-    for (int64_t x = b; x < E; x += 16) st16(L.ring + (x & (kRing - 1)), ld16_guarded(L.dst + x, L.oend - x));
+    for (int64_t x = L.F - 16; x < E; x += 16) {
+        if (x >= 0) st16(stage_at(L, x), ld16_guarded(L.dst + x, L.oend - x));
+    }
+}
+
+// Input window: make it cover [ip, ip + 32) (ip - ib < 32).
+__device__ __forceinline__ void win_sync(Lane& L) {
+    const int64_t d = L.ip - L.ib;
+    if (d < 32) return;
+    const bool shift = d < 64;
+    const int64_t nb = shift ? L.ib + 32 : (L.ip & ~(int64_t)15);
+    const int64_t first = shift ? nb + 32 : nb;
+    u32x4 k0 = u32x4{0, 0, 0, 0}, k1 = k0;
+    if (shift) {
+        k0 = ld16(L.win + 32);
+        k1 = ld16(L.win + 48);
+    }
+    u32x4 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int64_t x = nb + 16 * k;
+        v[k] = u32x4{0, 0, 0, 0};
+        if (x >= first) v[k] = x + 16 <= L.iend ? ld16(L.src + x) : ld16_guarded(L.src + x, L.iend - x);
+    }
+    if (shift) {
+        st16(L.win, k0);
+        st16(L.win + 16, k1);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (nb + 16 * k >= first) st16(L.win + 16 * k, v[k]);
+    }
+    L.ib = nb;
 }
 
 // ---------------------------------------------------------------- lane copies
@@ -313,37 +332,36 @@ __device__ __forceinline__ bool read_len(const uint8_t* src, int64_t& ip, int64_
     return true;
 }
 
-template <bool RING>
+template <bool STAGE>
 __device__ __forceinline__ void emit_literal(Lane& L, int64_t ip, int64_t op, int64_t lit, Copy& c,
                                              bool deferred) {
     if (lit == 0) return;
     if (deferred || lit > kCoopMin) {
         c = Copy{kLiteral, op, ip, lit};
-    } else if (RING) {
-        ring_literal(L, op, ip, lit);
+    } else if (STAGE) {
+        stage_literal(L, op, ip, lit);
     } else {
         lane_copy(L.dst + op, L.src + ip, lit, L.oend - op, L.iend - ip);
     }
 }
 
-template <bool RING>
+template <bool STAGE>
 __device__ __forceinline__ void emit_match(Lane& L, int64_t op, int64_t off, int64_t ml, Copy& c, bool deferred) {
     if (deferred || ml > kCoopMin) {
         c = Copy{kMatch, op, off, ml};
-    } else if (RING) {
-        ring_match(L, op, off, ml);
+    } else if (STAGE) {
+        stage_match(L, op, off, ml);
     } else {
         lane_match(L.dst + op, off, ml, L.oend - op);
     }
 }
 
 // Literal bytes 1..lit (lit <= 14) of the token window.
-template <bool RING>
+template <bool STAGE>
 __device__ __forceinline__ void window_literal(Lane& L, int64_t op, u32x4 w, int64_t lit) {
-    if (RING) {
-        if (lit == 0) return;
-        ring_sync(L, op);
-        ring_write(L.ring, op, window_shift1(w), (uint32_t)lit);
+    if (STAGE) {
+        stage_sync(L, op);
+        st16(stage_at(L, op), window_shift1(w));   // wild 16-byte store
     } else {
         st16(L.dst + op, window_shift1(w));   // wild 16-byte store, inside the oend-32 margin
     }
@@ -367,7 +385,7 @@ __device__ __noinline__ void dict_match(Lane& L, int64_t op, int64_t off, int64_
 }
 
 // One sequence of block L.  Deferred copies land in lc / mc.
-template <bool DICT, bool RING>
+template <bool DICT, bool STAGE>
 __device__ __forceinline__ void decode_step(Lane& L, Copy& lc, Copy& mc) {
     const u32x4 w = ld16_guarded(L.src + L.ip, L.iend - L.ip);
     const uint32_t tok = w.x & 0xFFu;
@@ -388,7 +406,7 @@ __device__ __forceinline__ void decode_step(Lane& L, Copy& lc, Copy& mc) {
                 L.fast = false;
                 goto literal_tail;
             }
-            emit_literal<RING>(L, ip, op, lit, lc, false);
+            emit_literal<STAGE>(L, ip, op, lit, lc, false);
             deferred = lc.kind != kNone;
             ip += lit;
             op += lit;
@@ -399,7 +417,7 @@ __device__ __forceinline__ void decode_step(Lane& L, Copy& lc, Copy& mc) {
                 goto literal_tail;
             }
             // literals are bytes 1..lit of the token window
-            window_literal<RING>(L, op, w, lit);
+            window_literal<STAGE>(L, op, w, lit);
             off = lit <= 13 ? (window_dword(w, (uint32_t)(1 + lit)) & 0xFFFFu) : ld16le(L.src + ip + lit);
             ip += lit;
             op += lit;
@@ -421,7 +439,7 @@ __device__ __forceinline__ void decode_step(Lane& L, Copy& lc, Copy& mc) {
                 goto match_tail;
             }
             if (off >= 8 && off <= op) {
-                emit_match<RING>(L, op, off, ml, mc, deferred);
+                emit_match<STAGE>(L, op, off, ml, mc, deferred);
                 op += ml;
                 goto done;
             }
@@ -434,21 +452,21 @@ __device__ __forceinline__ void decode_step(Lane& L, Copy& lc, Copy& mc) {
             op += ml;
             goto done;
         }
-        emit_match<RING>(L, op, off, ml, mc, deferred);
+        emit_match<STAGE>(L, op, off, ml, mc, deferred);
         op += ml;
         goto done;
     }
 
     // safe phase, lz4.c:2114-2329
     if (lit != 15 && ip < iend - 16 && op <= oend - 32) {   // shortcut, lz4.c:2128-2158
-        window_literal<RING>(L, op, w, lit);
+        window_literal<STAGE>(L, op, w, lit);
         off = lit <= 13 ? (window_dword(w, (uint32_t)(1 + lit)) & 0xFFFFu) : ld16le(L.src + ip + lit);
         op += lit;
         ip += lit + 2;
         ml = tok & 15;
         if (ml != 15 && off >= 8 && off <= op) {
-            if (RING) {
-                ring_match(L, op, off, ml + 4);
+            if (STAGE) {
+                stage_match(L, op, off, ml + 4);
             } else {
                 lane_match(L.dst + op, off, ml + 4, oend - op);
             }
@@ -464,14 +482,14 @@ __device__ __forceinline__ void decode_step(Lane& L, Copy& lc, Copy& mc) {
 literal_tail:   // lz4.c:2172-2229
     if (op + lit > oend - 12 || ip + lit > iend - 8) {
         if (ip + lit != iend || op + lit > oend) goto fail;
-        emit_literal<RING>(L, ip, op, lit, lc, false);   // last literals: exact (never past oend / iend)
+        emit_literal<STAGE>(L, ip, op, lit, lc, false);   // last literals: exact (never past oend / iend)
         op += lit;
         L.result = (int32_t)op;
         L.live = false;
         L.op = op;
         return;
     }
-    emit_literal<RING>(L, ip, op, lit, lc, false);
+    emit_literal<STAGE>(L, ip, op, lit, lc, false);
     deferred = lc.kind != kNone;
     ip += lit;
     op += lit;
@@ -494,7 +512,7 @@ match_tail:   // lz4.c:2248-2328
         goto done;
     }
     if (op + ml > oend - 5) goto fail;
-    emit_match<RING>(L, op, off, ml, mc, deferred);
+    emit_match<STAGE>(L, op, off, ml, mc, deferred);
     op += ml;
 done:
     L.ip = ip;
@@ -588,12 +606,12 @@ __global__ __launch_bounds__(256) void decompress_kernel(const uint8_t* __restri
 }
 
 
-// One round of wave-cooperative long copies in RING mode.  Each lane with a
-// copy [dpos, E) first writes the head up to the next 64-byte boundary A
-// through its ring and flushes, so [0, A) is in HBM; the wave then copies
+// One round of wave-cooperative long copies in STAGE mode.  Each lane with
+// a copy [dpos, E) first writes the head up to the next 64-byte boundary A
+// through its stage and flushes, so [0, A) is in HBM; the wave then copies
 // [A, E) of every such lane straight to HBM at wave width (lane order); the
-// lane finally restarts its ring from HBM at E.
-__device__ __forceinline__ void ring_coop(Lane& L, const Copy& c, uint32_t lane) {
+// lane finally restarts its stage from HBM at E.
+__device__ __forceinline__ void stage_coop(Lane& L, const Copy& c, uint32_t lane) {
     int64_t A = 0, E = 0;
     bool coop = false;
     if (c.kind != kNone) {
@@ -602,13 +620,13 @@ __device__ __forceinline__ void ring_coop(Lane& L, const Copy& c, uint32_t lane)
         A = up < E ? up : E;
         if (A > c.dpos) {
             if (c.kind == kLiteral) {
-                ring_literal(L, c.dpos, c.arg, A - c.dpos);
+                stage_literal(L, c.dpos, c.arg, A - c.dpos);
             } else {
-                ring_match(L, c.dpos, c.arg, A - c.dpos);
+                stage_match(L, c.dpos, c.arg, A - c.dpos);
             }
         }
         if (A < E) {
-            while (L.F + 64 <= A) ring_flush(L);
+            while (L.F + 64 <= A) stage_flush(L);
             coop = true;
         }
     }
@@ -631,60 +649,149 @@ __device__ __forceinline__ void ring_coop(Lane& L, const Copy& c, uint32_t lane)
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     }
-    if (coop) ring_reload(L, E);
+    if (coop) stage_reload(L, E);
 }
 
-// Independent blocks without a dictionary (the hot path).  Same lane-per-
-// block state machine as decompress_kernel, output through the LDS ring.
-__global__ __launch_bounds__(256) void ring_decompress_kernel(const uint8_t* __restrict__ src,
-                                                              const int64_t* __restrict__ src_off,
-                                                              const int32_t* __restrict__ src_len, uint8_t* dst,
-                                                              const int64_t* __restrict__ dst_off,
-                                                              const int32_t* __restrict__ dst_cap,
-                                                              int32_t* __restrict__ status, int64_t n) {
-    __shared__ __attribute__((aligned(16))) uint8_t rings[256 * kRing];
+// ---------------------------------------------------------------- fast path
+// The common sequence, in the reference's fast loop (lz4.c:1996-2109):
+// literal length <= 12 (literal and offset inside the 16-byte token window),
+// at most one extra match-length byte, offset >= 16 and within the output,
+// match <= 64 bytes, and both the literal and the match take the in-loop
+// branches (ip <= iend - 17 after the token; op + ml < oend - 64; the
+// match-length read stays below iend - 4).  Such a sequence cannot fail and
+// is decoded exactly as decode_step would; anything else takes decode_step.
+struct FastSeq {
+    int64_t lit, off, ml, ipn;
+};
+
+__device__ __forceinline__ bool fast_seq(const Lane& L, u32x4 w, FastSeq& f) {
+    const uint32_t tok = w.x & 0xFFu;
+    const int64_t lit = tok >> 4, mlc = tok & 15;
+    const int64_t ip1 = L.ip + 1;
+    if (!L.fast || lit > 12 || ip1 > L.iend - 17) return false;
+    const int64_t off = window_dword(w, (uint32_t)(1 + lit)) & 0xFFFFu;
+    int64_t ml = mlc + 4, ipn = ip1 + lit + 2;
+    if (mlc == 15) {   // read_len (lz4.c:1903-1928) with a single byte < 255
+        const int64_t b = byte_of(w, (int)(3 + lit));
+        if (b == 255 || ipn + 1 > L.iend - 4) return false;
+        ml = 19 + b;
+        ipn += 1;
+    }
+    const int64_t opm = L.op + lit;
+    if (off < 16 || off > opm || ml > kCoopMin || opm + ml >= L.oend - 64) return false;
+    f = FastSeq{lit, off, ml, ipn};
+    return true;
+}
+
+__device__ __forceinline__ void fast_exec(Lane& L, u32x4 w, const FastSeq& f) {
+    st16(stage_at(L, L.op), window_shift1(w));   // literals (wild), op < F + 64
+    const int64_t opm = L.op + f.lit;
+    for (int64_t i = 0; i < f.ml; i += 16) {
+        stage_sync(L, opm + i);
+        st16(stage_at(L, opm + i), out_read16(L, opm + i - f.off));
+    }
+    L.ip = f.ipn;
+    L.op = opm + f.ml;
+}
+
+// Independent blocks without a dictionary (the hot path): one lane per block,
+// LDS-staged input and output.  Each iteration every live lane classifies its
+// next sequence; the wave runs a fast step for the fast-path lanes, or -- once
+// `slow_batch` lanes wait (or none can go fast) -- one general decode_step
+// for the waiting lanes.  Batching keeps the rarely needed general state
+// machine (and its divergence) off most iterations.
+__global__ __launch_bounds__(256) void stage_decompress_kernel(const uint8_t* __restrict__ src,
+                                                               const int64_t* __restrict__ src_off,
+                                                               const int32_t* __restrict__ src_len, uint8_t* dst,
+                                                               const int64_t* __restrict__ dst_off,
+                                                               const int32_t* __restrict__ dst_cap,
+                                                               int32_t* __restrict__ status, int64_t n,
+                                                               unsigned long long* __restrict__ next,
+                                                               int32_t slow_batch) {
+    __shared__ __attribute__((aligned(16))) uint8_t stages[256 * kStage];
+    __shared__ __attribute__((aligned(16))) uint8_t wins[256 * kWin];
     const uint32_t lane = lane_id();
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     Lane L;
     L.live = false;
     L.result = -1;
-    L.ring = rings + threadIdx.x * kRing;
+    L.stage = stages + threadIdx.x * kStage;
+    L.win = wins + threadIdx.x * kWin;
+    L.ip = 0;
+    L.op = 0;
     L.F = 0;
-    bool open = false;   // ring holds output not yet in HBM
-    if (i < n) {
-        L.src = src + src_off[i];
-        L.dst = dst + dst_off[i];
-        L.iend = src_len[i];
-        L.oend = dst_cap[i];
-        L.ip = 0;
-        L.op = 0;
-        L.dict_len = 0;
-        L.dict_end = nullptr;
-        if (L.oend < 0) {
-            L.result = -1;   // lz4.c:1950
-        } else if (L.oend == 0) {
-            L.result = (L.iend == 1 && L.src[0] == 0) ? 0 : -1;   // lz4.c:1978-1982
-        } else if (L.iend <= 0) {
-            L.result = -1;   // lz4.c:1983
-        } else {
-            L.fast = L.oend >= 64;
-            L.live = true;
-            open = true;
+    L.ib = 0;
+    L.dict_len = 0;
+    L.dict_end = nullptr;
+    int64_t idx = -1;    // block this lane decodes
+    bool more = true;    // wave-uniform: the queue may still hold blocks
+    while (true) {
+        // idle lanes take the next blocks: one atomic per wave and refill
+        if (more) {
+            const uint64_t need = __ballot(!L.live);
+            if (need != 0) {
+                const int first = __builtin_ctzll(need);
+                const uint32_t cnt = (uint32_t)__popcll(need);
+                unsigned long long base = 0;
+                if ((int)lane == first) base = atomicAdd(next, (unsigned long long)cnt);
+                base = (unsigned long long)readlane64((int64_t)base, first);
+                if (base + cnt >= (unsigned long long)n) more = false;
+                if (!L.live) {
+                    const uint64_t below = lane == 0 ? 0 : (need & (~0ull >> (64 - lane)));
+                    idx = (int64_t)(base + (unsigned long long)__popcll(below));
+                    if (idx < n) {
+                        L.src = src + src_off[idx];
+                        L.dst = dst + dst_off[idx];
+                        L.iend = src_len[idx];
+                        L.oend = dst_cap[idx];
+                        L.ip = 0;
+                        L.op = 0;
+                        L.F = 0;
+                        L.ib = -2 * kWin;
+                        if (L.oend < 0) {
+                            status[idx] = -1;   // lz4.c:1950
+                        } else if (L.oend == 0) {
+                            status[idx] = (L.iend == 1 && L.src[0] == 0) ? 0 : -1;   // lz4.c:1978-1982
+                        } else if (L.iend <= 0) {
+                            status[idx] = -1;   // lz4.c:1983
+                        } else {
+                            L.fast = L.oend >= 64;
+                            L.live = true;
+                        }
+                    }
+                }
+            }
+        }
+        if (!__any(L.live)) {
+            if (more) continue;
+            break;
+        }
+        FastSeq f{0, 0, 0, 0};
+        u32x4 w = u32x4{0, 0, 0, 0};
+        bool fok = false;
+        if (L.live) {
+            win_sync(L);
+            stage_sync(L, L.op);
+            w = ld16(L.win + (L.ip - L.ib));
+            fok = fast_seq(L, w, f);
+        }
+        const uint64_t fm = __ballot(fok);
+        const uint64_t sm = __ballot(L.live && !fok);
+        if (sm != 0 && (fm == 0 || __popcll(sm) >= (uint32_t)slow_batch)) {
+            Copy lc{kNone, 0, 0, 0}, mc{kNone, 0, 0, 0};
+            const bool stepped = L.live && !fok;
+            if (stepped) decode_step<false, true>(L, lc, mc);
+            if (__ballot(lc.kind != kNone || mc.kind != kNone)) {
+                stage_coop(L, lc, lane);   // literal before match
+                stage_coop(L, mc, lane);
+            }
+            if (stepped && !L.live) {   // block finished (or failed)
+                stage_finish(L, L.result >= 0 ? (int64_t)L.result : L.op);
+                status[idx] = L.result;
+            }
+        } else if (fok) {
+            fast_exec(L, w, f);
         }
     }
-    while (__any(L.live)) {
-        Copy lc{kNone, 0, 0, 0}, mc{kNone, 0, 0, 0};
-        if (L.live) decode_step<false, true>(L, lc, mc);
-        if (__ballot(lc.kind != kNone || mc.kind != kNone)) {
-            ring_coop(L, lc, lane);   // literal before match
-            ring_coop(L, mc, lane);
-        }
-        if (open && !L.live) {
-            ring_finish(L, L.result >= 0 ? (int64_t)L.result : L.op);
-            open = false;
-        }
-    }
-    if (i < n) status[i] = L.result;
 }
 
 // Linked-block frames (lz4frame.c:1853-1856, LZ4F_updateDict): block i may
@@ -770,25 +877,79 @@ __global__ __launch_bounds__(64) void decompress_chain_kernel(const uint8_t* __r
 
 using namespace lz4m;
 
-extern "C" int lz4m_decompress_batch(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len,
-                                     uint8_t* d_dst, const int64_t* d_dst_off, const int32_t* d_dst_cap,
-                                     int32_t* d_status, int64_t n, lz4m_stream_t stream) {
+namespace {
+
+// Persistent grid for the staged decoder: every resident workgroup slot of
+// the device, no more (blocks come from the work queue).
+int64_t stage_grid(int64_t n) {
+    static const int64_t slots = [] {
+        int dev = 0, cus = 0, per_cu = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(lz4m::stage_decompress_kernel),
+                                                           256, 0);
+        const int64_t s = (int64_t)(cus > 0 ? cus : 256) * (per_cu > 0 ? per_cu : 1);
+        return s;
+    }();
+    const int64_t need = (n + 255) / 256;
+    return need < slots ? need : slots;
+}
+
+int env_int(const char* name, int dflt) {
+    const char* e = getenv(name);
+    const int v = e != nullptr ? atoi(e) : 0;
+    return v > 0 ? v : dflt;
+}
+
+}  // namespace
+
+extern "C" size_t lz4m_decompress_workspace_bytes(void) { return 64; }
+
+extern "C" int lz4m_decompress_batch_ws(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len,
+                                        uint8_t* d_dst, const int64_t* d_dst_off, const int32_t* d_dst_cap,
+                                        int32_t* d_status, int64_t n, void* d_work, size_t work_bytes,
+                                        lz4m_stream_t stream) {
     if (n < 0) return LZ4M_EINVAL;
     if (n == 0) return 0;
-    const int64_t grid = (n + 255) / 256;
-    // LZ4M_DECODER=direct selects the ring-less kernel (A/B measurements only)
+    // LZ4M_DECODER=direct selects the unstaged kernel (A/B measurements only)
     static const bool direct = [] {
         const char* e = getenv("LZ4M_DECODER");
         return e != nullptr && strcmp(e, "direct") == 0;
     }();
     if (direct) {
+        const int64_t grid = (n + 255) / 256;
         hipLaunchKernelGGL(decompress_kernel<false>, dim3((uint32_t)grid), dim3(256), 0, (hipStream_t)stream, d_src,
                            d_src_off, d_src_len, d_dst, d_dst_off, d_dst_cap, nullptr, nullptr, nullptr, d_status, n);
-    } else {
-        hipLaunchKernelGGL(ring_decompress_kernel, dim3((uint32_t)grid), dim3(256), 0, (hipStream_t)stream, d_src,
-                           d_src_off, d_src_len, d_dst, d_dst_off, d_dst_cap, d_status, n);
+        return (int)hipGetLastError();
     }
+    if (d_work == nullptr || work_bytes < lz4m_decompress_workspace_bytes() || ((uintptr_t)d_work & 7) != 0)
+        return LZ4M_EINVAL;
+    // LZ4M_SLOW_BATCH: waiting lanes that trigger a general step (tuning)
+    static const int slow_batch = env_int("LZ4M_SLOW_BATCH", 8);
+    hipError_t e = hipMemsetAsync(d_work, 0, sizeof(unsigned long long), (hipStream_t)stream);
+    if (e != hipSuccess) return (int)e;
+    hipLaunchKernelGGL(stage_decompress_kernel, dim3((uint32_t)stage_grid(n)), dim3(256), 0, (hipStream_t)stream,
+                       d_src, d_src_off, d_src_len, d_dst, d_dst_off, d_dst_cap, d_status, n,
+                       static_cast<unsigned long long*>(d_work), slow_batch);
     return (int)hipGetLastError();
+}
+
+extern "C" int lz4m_decompress_batch(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len,
+                                     uint8_t* d_dst, const int64_t* d_dst_off, const int32_t* d_dst_cap,
+                                     int32_t* d_status, int64_t n, lz4m_stream_t stream) {
+    if (n < 0) return LZ4M_EINVAL;
+    if (n == 0) return 0;
+    // library-owned queue counters, used round-robin (one per call in flight)
+    constexpr int kSlots = 1024;
+    static unsigned long long* pool = nullptr;
+    static std::atomic<uint32_t> turn{0};
+    static std::once_flag once;
+    static hipError_t pool_err = hipSuccess;
+    std::call_once(once, [] { pool_err = hipMalloc(reinterpret_cast<void**>(&pool), 64 * kSlots); });
+    if (pool_err != hipSuccess) return (int)pool_err;
+    unsigned long long* slot = pool + 8 * (turn.fetch_add(1) % kSlots);
+    return lz4m_decompress_batch_ws(d_src, d_src_off, d_src_len, d_dst, d_dst_off, d_dst_cap, d_status, n, slot, 64,
+                                    stream);
 }
 
 extern "C" int lz4m_decompress_batch_dict(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len,

@@ -34,6 +34,8 @@ def _declare(lib) -> None:
         "lz4m_version_number": ([], i32),
         "lz4m_version_string": ([], C.c_char_p),
         "lz4m_decompress_batch": ([vp, vp, vp, vp, vp, vp, vp, i64, vp], i32),
+        "lz4m_decompress_workspace_bytes": ([], C.c_size_t),
+        "lz4m_decompress_batch_ws": ([vp, vp, vp, vp, vp, vp, vp, i64, vp, C.c_size_t, vp], i32),
         "lz4m_decompress_batch_dict": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, vp], i32),
         "lz4m_decompress_chain": ([vp, vp, vp, vp, vp, vp, i64, i32, vp], i32),
         "lz4m_compress_batch": ([vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, vp], i32),
@@ -98,13 +100,28 @@ def launch_decompress(src, src_off, src_len, dst, dst_off, dst_cap, status, n, s
     L = lib()
     sp = stream_ptr(stream)
     if dict_buf is None:
-        rc = L.lz4m_decompress_batch(ptr(src), ptr(src_off), ptr(src_len), ptr(dst), ptr(dst_off), ptr(dst_cap),
-                                     ptr(status), n, sp)
+        work = _workspace(src.device, sp)
+        rc = L.lz4m_decompress_batch_ws(ptr(src), ptr(src_off), ptr(src_len), ptr(dst), ptr(dst_off), ptr(dst_cap),
+                                        ptr(status), n, ptr(work), work.numel(), sp)
     else:
         rc = L.lz4m_decompress_batch_dict(ptr(src), ptr(src_off), ptr(src_len), ptr(dst), ptr(dst_off),
                                           ptr(dst_cap), ptr(dict_buf), ptr(dict_off), ptr(dict_len), ptr(status),
                                           n, sp)
     check(rc, "lz4m_decompress_batch")
+
+
+_WORK = {}
+
+
+def _workspace(dev, sp) -> torch.Tensor:
+    """Decoder scratch (work-queue counter), one per (device, stream): calls
+    on one stream are ordered, so they can share it."""
+    key = (dev, sp)
+    w = _WORK.get(key)
+    if w is None:
+        w = torch.empty(int(lib().lz4m_decompress_workspace_bytes()), dtype=torch.uint8, device=dev)
+        _WORK[key] = w
+    return w
 
 
 def launch_decompress_chain(src, src_off, src_len, raw_mask, dst, status, n, max_block, stream=None) -> None:
