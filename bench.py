@@ -144,6 +144,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-compress", action="store_true")
     ap.add_argument("--random-blocks", type=int, default=1 << 17, help="blocks of the random-data extra line")
+    ap.add_argument("--e2e-blocks", type=int, default=1 << 15,
+                    help="blocks of the host-to-host (PCIe-inclusive) extra line; 0 = skip")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -206,8 +208,29 @@ def main():
     if not (ok_status and ok_bytes):
         raise SystemExit(f"decompress verification failed: status_ok={ok_status} bytes_ok={ok_bytes}")
 
-    # ---- extra: incompressible (random) blocks ----
+    # ---- extra: end to end from pinned host memory (PCIe-inclusive) ----
     extra = {}
+    if args.e2e_blocks > 0:
+        ne = min(args.e2e_blocks, n)
+        e_comp_bytes = int(c_off[ne - 1]) + int(c_len[ne - 1]) if ne < n else comp_total
+        h_comp = torch.empty(e_comp_bytes, dtype=torch.uint8, pin_memory=True)
+        h_comp.copy_(comp[:e_comp_bytes])
+        h_out = torch.empty(ne * BLOCK, dtype=torch.uint8, pin_memory=True)
+        e_in = torch.empty(e_comp_bytes, dtype=torch.uint8, device=dev)
+        e_st = torch.empty(ne, dtype=torch.int32, device=dev)
+
+        def do_e2e():
+            e_in.copy_(h_comp, non_blocking=True)
+            N.launch_decompress(e_in, c_off[:ne], c_len[:ne], dst, dst_off[:ne], dst_cap[:ne], e_st, ne)
+            h_out.copy_(dst[: ne * BLOCK], non_blocking=True)
+
+        e_wall, _ = time_kernel(do_e2e, max(1, args.steps // 2), 1, world)
+        assert bool((e_st == BLOCK).all()) and torch.equal(h_out[: 4 * BLOCK], src[: 4 * BLOCK].cpu())
+        extra["end_to_end_host_gib_s"] = round(world * ne * BLOCK / (e_wall / max(1, args.steps // 2)) / GIB, 2)
+        extra["end_to_end_blocks"] = ne
+        del h_comp, h_out, e_in, e_st
+
+    # ---- extra: incompressible (random) blocks ----
     if args.random_blocks > 0:
         del dst
         torch.cuda.empty_cache()
@@ -232,13 +255,18 @@ def main():
     value = world * n * BLOCK / d_step / GIB
     algo_bytes = comp_total + n * BLOCK          # per launch: read compressed + write decoded
     achieved = algo_bytes / d_ev / 1e9           # GB/s, from HIP events on the launch stream
+    # HBM bytes per launch of the decoder from the committed PMC summary of
+    # this same command (tools/pmc_bench.sh -> profiles/pmc_decompress.json),
+    # used only when it was measured on this configuration
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_decompress.json")
     if os.path.exists(pmc_path):
         try:
             with open(pmc_path) as f:
-                traffic = json.load(f).get("hbm_bytes_per_launch")
-        except Exception:
+                pmc = json.load(f)
+            if pmc.get("blocks") == n and pmc.get("pool") == args.pool:
+                traffic = pmc.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
             traffic = None
     res = {
         "metric": "GiB/s uncompressed, device-resident, 64 KiB blocks (decompress; compress)",
