@@ -144,6 +144,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-compress", action="store_true")
     ap.add_argument("--random-blocks", type=int, default=1 << 17, help="blocks of the random-data extra line")
+    ap.add_argument("--gather-blocks", type=int, default=1 << 16,
+                    help="N>1: compressed blocks per rank gathered at rank 0 over RCCL (config 5 exchange)")
     ap.add_argument("--e2e-blocks", type=int, default=1 << 15,
                     help="blocks of the host-to-host (PCIe-inclusive) extra line; 0 = skip")
     args = ap.parse_args()
@@ -208,8 +210,30 @@ def main():
     if not (ok_status and ok_bytes):
         raise SystemExit(f"decompress verification failed: status_ok={ok_status} bytes_ok={ok_bytes}")
 
-    # ---- extra: end to end from pinned host memory (PCIe-inclusive) ----
     extra = {}
+    # ---- extra (N > 1): gather compressed shards at rank 0 over RCCL ----
+    if world > 1 and args.gather_blocks > 0:
+        from lz4._dist import gather_compressed
+        ng = min(args.gather_blocks, n)
+        g_bytes = int(c_off[ng - 1]) + int(c_len[ng - 1])
+        g_comp, g_len = comp[:g_bytes], c_len[:ng]
+        box = {}
+
+        def do_gather():
+            box["r"] = gather_compressed(g_comp, g_len, root=0)
+
+        g_wall, _ = time_kernel(do_gather, 1, 1, world)
+        tot = torch.tensor([g_bytes], dtype=torch.int64, device=dev)
+        torch.distributed.all_reduce(tot)
+        if rank == 0:
+            buf, _, lens = box["r"]
+            assert buf.numel() == int(tot) and lens.numel() == world * ng
+            assert torch.equal(buf[:g_bytes], g_comp)
+        extra["gather_compressed_gb_s"] = round(int(tot) / g_wall / 1e9, 2)
+        extra["gather_blocks_per_rank"] = ng
+        box.clear()
+
+    # ---- extra: end to end from pinned host memory (PCIe-inclusive) ----
     if args.e2e_blocks > 0:
         ne = min(args.e2e_blocks, n)
         e_comp_bytes = int(c_off[ne - 1]) + int(c_len[ne - 1]) if ne < n else comp_total
