@@ -42,6 +42,11 @@ typedef struct ihipStream_t* lz4m_stream_t;   /* == hipStream_t */
 #define LZ4M_TABLE_U32_HASH5 1
 /* pick what LZ4_compress_default would pick for each block's size */
 #define LZ4M_TABLE_AUTO      2
+/* parallel-parse compressor (lz4m_pcompress.hip): a valid block at the ratio
+ * of LZ4_compress_default (greedy, full insertion, catch-up), NOT
+ * byte-identical to it; blocks up to 64 KiB (larger ones get size 0);
+ * `acceleration` is ignored.  For bulk compression (BASELINE config 3). */
+#define LZ4M_PARSE_PARALLEL  3
 
 /* LZ4_compressBound (lz4.h:212 / lz4.c:730). */
 int lz4m_compress_bound(int input_size);

@@ -21,6 +21,7 @@ LIB_PATH = os.path.join(_HERE, "_lz4m.so")
 TABLE_U16_HASH4 = 0
 TABLE_U32_HASH5 = 1
 TABLE_AUTO = 2
+PARSE_PARALLEL = 3   # parallel-parse compressor: valid blocks, ratio of LZ4_compress_default
 EINVAL = 0x10000
 
 _lock = threading.Lock()

@@ -215,3 +215,54 @@ def test_scan_and_gather(gpu):
         offs = N.exclusive_scan(t, add=3, base=11).cpu().numpy()
         want = np.concatenate([[0], np.cumsum(lens.astype(np.int64) + 3)]) + 11
         assert (offs == want).all(), n
+
+
+# ---------------------------------------------------------------- parallel parse
+def _decodes(oracle, comp, plain):
+    st, out = oracle.decompress(comp, len(plain))
+    return st == len(plain) and out == plain
+
+
+def test_parallel_parse_valid(gpu, oracle, corpus):
+    """Every block the parallel-parse compressor emits is a valid LZ4 block
+    that the reference decoder (oracle, pinned to lz4libs) decodes exactly."""
+    blocks, ragged = corpus
+    src = blocks + ragged + [bytes(65536), bytes([7]) * 65536, b"ab" * 32768, b"abc" * 21845,
+                             bytes(range(256)) * 256]
+    got = gpu_compress(src, N.PARSE_PARALLEL, gpu)
+    for i, b in enumerate(src):
+        assert got[i] is not None and len(got[i]) <= N.compress_bound(len(b)), i
+        assert _decodes(oracle, got[i], b), (i, len(b))
+
+
+@pytest.mark.parametrize("kind", ["text", "source", "records", "markup", "runs", "random", "silesia"])
+def test_parallel_parse_ratio(gpu, oracle, kind):
+    """Ratio within 5 % of LZ4_compress_default (BASELINE config 3), per kind."""
+    src = [b.tobytes() for b in _synth.blocks(24, kind, seed=31)]
+    got = gpu_compress(src, N.PARSE_PARALLEL, gpu)
+    ours = sum(len(g) for g in got)
+    ref = sum(len(oracle.compress(b)) for b in src)
+    assert ours <= 1.05 * ref, (kind, ours, ref)
+    for g, b in zip(got, src):
+        assert _decodes(oracle, g, b)
+
+
+def test_parallel_parse_limited_output(gpu, oracle, corpus):
+    blocks, _ = corpus
+    noise = np.random.default_rng(3).integers(0, 256, 65536, dtype=np.uint8).tobytes()
+    src = blocks[:24] + [bytes(range(256)) * 256, noise]
+    caps = [len(b) - 1 for b in src]
+    got = gpu_compress(src, N.PARSE_PARALLEL, gpu, caps=caps)
+    for i, b in enumerate(src):
+        if got[i] is not None:
+            assert len(got[i]) <= caps[i] and _decodes(oracle, got[i], b), i
+    assert got[-1] is None   # incompressible block does not fit size - 1
+
+
+def test_parallel_parse_decoded_by_gpu(gpu, corpus):
+    blocks, ragged = corpus
+    src = blocks[:32] + ragged
+    got = gpu_compress(src, N.PARSE_PARALLEL, gpu)
+    res = gpu_decompress(got, [len(b) for b in src], gpu)
+    for i, (s, out) in enumerate(res):
+        assert s == len(src[i]) and out == src[i], i
