@@ -47,6 +47,9 @@ typedef struct ihipStream_t* lz4m_stream_t;   /* == hipStream_t */
  * byte-identical to it; blocks up to 64 KiB (larger ones get size 0);
  * `acceleration` is ignored.  For bulk compression (BASELINE config 3). */
 #define LZ4M_PARSE_PARALLEL  3
+/* the same parse for blocks of any size (32 KiB LDS table of u32 positions,
+ * offsets limited to 65535 like LZ4_DISTANCE_MAX); e.g. 4 MiB frame blocks */
+#define LZ4M_PARSE_PARALLEL_LARGE 4
 
 /* LZ4_compressBound (lz4.h:212 / lz4.c:730). */
 int lz4m_compress_bound(int input_size);

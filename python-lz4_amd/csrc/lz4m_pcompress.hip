@@ -48,6 +48,66 @@ __device__ __forceinline__ uint32_t eq_prefix16(u32x4 a, u32x4 b) {
 
 __device__ __forceinline__ int32_t rdl(int32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
 
+// v of lane (lane ^ j), j a power of two, without the LDS crossbar: DPP
+// within 16-lane rows (quad_perm, row_shl/shr, row_ror), gfx950 permlane
+// swaps across rows and halves.
+template <int J>
+__device__ __forceinline__ uint32_t xor_lane(uint32_t v, uint32_t lane) {
+    const int x = (int)v;
+    if constexpr (J == 1) {
+        return (uint32_t)__builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, false);   // quad_perm:[1,0,3,2]
+    } else if constexpr (J == 2) {
+        return (uint32_t)__builtin_amdgcn_mov_dpp(x, 0x4E, 0xF, 0xF, false);   // quad_perm:[2,3,0,1]
+    } else if constexpr (J == 4) {
+        const int up = __builtin_amdgcn_update_dpp(x, x, 0x104, 0xF, 0xF, false);   // row_shl:4: lane + 4
+        const int dn = __builtin_amdgcn_update_dpp(x, x, 0x114, 0xF, 0xF, false);   // row_shr:4: lane - 4
+        return (uint32_t)((lane & 4) ? dn : up);
+    } else if constexpr (J == 8) {
+        return (uint32_t)__builtin_amdgcn_mov_dpp(x, 0x128, 0xF, 0xF, false);   // row_ror:8
+    } else if constexpr (J == 16) {
+        const auto p = __builtin_amdgcn_permlane16_swap((unsigned)x, (unsigned)x, false, false);
+        return (lane & 16) ? p[0] : p[1];
+    } else {
+        const auto p = __builtin_amdgcn_permlane32_swap((unsigned)x, (unsigned)x, false, false);
+        return (lane & 32) ? p[0] : p[1];
+    }
+}
+
+// one bitonic compare-exchange stage (block size K, distance J)
+template <int K, int J>
+__device__ __forceinline__ uint32_t bitonic_stage(uint32_t key, uint32_t lane) {
+    const uint32_t other = xor_lane<J>(key, lane);
+    const bool up = (lane & K) == 0;
+    const bool lower = (lane & J) == 0;
+    return (lower == up) ? (key < other ? key : other) : (key > other ? key : other);
+}
+
+// ascending sort of one key per lane across the wave
+__device__ __forceinline__ uint32_t wave_sort(uint32_t key, uint32_t lane) {
+    key = bitonic_stage<2, 1>(key, lane);
+    key = bitonic_stage<4, 2>(key, lane);
+    key = bitonic_stage<4, 1>(key, lane);
+    key = bitonic_stage<8, 4>(key, lane);
+    key = bitonic_stage<8, 2>(key, lane);
+    key = bitonic_stage<8, 1>(key, lane);
+    key = bitonic_stage<16, 8>(key, lane);
+    key = bitonic_stage<16, 4>(key, lane);
+    key = bitonic_stage<16, 2>(key, lane);
+    key = bitonic_stage<16, 1>(key, lane);
+    key = bitonic_stage<32, 16>(key, lane);
+    key = bitonic_stage<32, 8>(key, lane);
+    key = bitonic_stage<32, 4>(key, lane);
+    key = bitonic_stage<32, 2>(key, lane);
+    key = bitonic_stage<32, 1>(key, lane);
+    key = bitonic_stage<64, 32>(key, lane);
+    key = bitonic_stage<64, 16>(key, lane);
+    key = bitonic_stage<64, 8>(key, lane);
+    key = bitonic_stage<64, 4>(key, lane);
+    key = bitonic_stage<64, 2>(key, lane);
+    key = bitonic_stage<64, 1>(key, lane);
+    return key;
+}
+
 __device__ __forceinline__ int32_t ext_len(int32_t x) { return x >= 15 ? 1 + (x - 15) / 255 : 0; }
 
 // Wave-cooperative forward match length of s[a..] vs s[c..] (c < a), at most
@@ -61,7 +121,6 @@ __device__ __forceinline__ int32_t wave_count(const uint8_t* s, int32_t a, int32
             e = x ? (int32_t)(__builtin_ctz(x) >> 3) : 4;
             const int32_t nb = lim - k < 4 ? lim - k : 4;
             if (e > nb) e = nb;
-            if (nb < 4 && e == nb) e = nb;   // reached the limit inside this dword
         }
         const bool full = k + 4 <= lim && e == 4;
         const uint64_t stop = __ballot(!full);
@@ -75,32 +134,41 @@ __device__ __forceinline__ int32_t wave_count(const uint8_t* s, int32_t a, int32
 // Encode `ns` sequences (lane s < ns holds lstart/lit/off/ml of sequence s;
 // ml == 0 marks the final literals-only sequence) at d + op, byte-parallel.
 // Returns the bytes written, or -1 if they do not fit before cap.
+__device__ __forceinline__ int32_t seq_size(int32_t lit, int32_t ml) {
+    return 1 + ext_len(lit) + lit + (ml ? 2 + ext_len(ml - 4) : 0);
+}
+
+constexpr int32_t kLongLit = 64;   // literals at least this long are copied 16 B per lane
+
+// Encode the ns sequences held in lanes 0..ns-1 (ml == 0 marks the final
+// literals-only sequence) at d + op.  obase = output offset of the sequence;
+// pbase = its first index in the "byte-parallel" space, which holds every
+// output byte except the literals of long-literal sequences (those are
+// copied by the whole wave, 16 bytes per lane).  Short-literal bytes come
+// from the registers of the current / previous 64-position chunk (v0 / vprev,
+// byte 0 of lane q - p0 is s[q]) when in reach, else from memory.
 __device__ __forceinline__ int32_t emit_seqs(const uint8_t* s, uint8_t* d, int32_t op, int32_t cap, int ns,
-                                             int32_t lstart, int32_t lit, int32_t off, int32_t ml, uint32_t lane) {
-    const bool v = (int)lane < ns;
-    const int32_t el = v ? ext_len(lit) : 0;
-    const int32_t em = v && ml ? ext_len(ml - 4) : 0;
-    const int32_t size = v ? 1 + el + lit + (ml ? 2 + em : 0) : 0;
-    // inclusive wave prefix sum
-    int32_t inc = size;
-#pragma unroll
-    for (int k = 1; k < 64; k <<= 1) {
-        const int32_t y = __shfl_up(inc, k);
-        if ((int)lane >= k) inc += y;
-    }
-    const int32_t base = inc - size;
-    const int32_t total = rdl(inc, ns - 1);
+                                             int32_t lstart, int32_t lit, int32_t off, int32_t ml, int32_t obase,
+                                             int32_t pbase, int32_t total, int32_t ptotal, int32_t p0, uint32_t v0,
+                                             uint32_t vprev, uint32_t lane) {
     if (op + total > cap) return -1;
-    for (int32_t t0 = 0; t0 < total; t0 += 64) {
+    for (int32_t t0 = 0; t0 < ptotal; t0 += 64) {
         const int32_t t = t0 + (int32_t)lane;
         int sq = 0;
         for (int k = 1; k < ns; ++k)
-            if (t >= rdl(base, k)) sq = k;
-        const int32_t b = __shfl(base, sq), L = __shfl(lit, sq), O = __shfl(off, sq), M = __shfl(ml, sq),
-                      S = __shfl(lstart, sq);
-        if (t < total) {
-            const int32_t r = t - b;
-            const int32_t EL = ext_len(L);
+            if (t >= rdl(pbase, k)) sq = k;
+        const int32_t pb = __shfl(pbase, sq), ob = __shfl(obase, sq), L = __shfl(lit, sq), O = __shfl(off, sq),
+                      M = __shfl(ml, sq), S = __shfl(lstart, sq);
+        const int32_t EL = ext_len(L);
+        const bool longlit = L >= kLongLit;
+        int32_t r = t - pb;                 // index within the sequence's byte-parallel part
+        if (longlit && r > EL) r += L;      // skip the wave-copied literals
+        // literal byte source (register window or memory)
+        const int32_t q = S + (r - 1 - EL);
+        const int32_t rel = q - p0;
+        const uint32_t w0 = (uint32_t)__builtin_amdgcn_ds_bpermute((rel & 63) << 2, (int)v0);
+        const uint32_t w1 = (uint32_t)__builtin_amdgcn_ds_bpermute((rel & 63) << 2, (int)vprev);
+        if (t < ptotal) {
             uint32_t byte;
             if (r == 0) {
                 const int32_t ln = L < 15 ? L : 15;
@@ -109,7 +177,7 @@ __device__ __forceinline__ int32_t emit_seqs(const uint8_t* s, uint8_t* d, int32
             } else if (r <= EL) {
                 byte = r < EL ? 255u : (uint32_t)((L - 15) % 255);
             } else if (r <= EL + L) {
-                byte = s[S + (r - 1 - EL)];
+                byte = rel >= 0 && rel < 64 ? (w0 & 0xFFu) : rel >= -64 && rel < 0 ? (w1 & 0xFFu) : s[q];
             } else if (r == EL + L + 1) {
                 byte = (uint32_t)(O & 0xFF);
             } else if (r == EL + L + 2) {
@@ -119,93 +187,148 @@ __device__ __forceinline__ int32_t emit_seqs(const uint8_t* s, uint8_t* d, int32
                 const int32_t k = r - (EL + L + 3);
                 byte = k < EM - 1 ? 255u : (uint32_t)((M - 4 - 15) % 255);
             }
-            d[op + t] = (uint8_t)byte;
+            d[op + ob + r] = (uint8_t)byte;
+        }
+    }
+    // long literals: coalesced 16-byte-per-lane copies
+    for (int k = 0; k < ns; ++k) {
+        const int32_t L = rdl(lit, k);
+        if (L < kLongLit) continue;
+        const int32_t S = rdl(lstart, k);
+        uint8_t* o = d + op + rdl(obase, k) + 1 + ext_len(L);
+        for (int32_t x = 16 * (int32_t)lane; x < L; x += 16 * 64) {
+            if (x + 16 <= L) {
+                st16(o + x, ld16(s + S + x));
+            } else {
+                for (int32_t y = x; y < L; ++y) o[y] = s[S + y];
+            }
         }
     }
     return total;
 }
 
+// Bytes [p, p + 4) as a little-endian word, zero past n.
+__device__ __forceinline__ uint32_t load_word(const uint8_t* s, int32_t p, int32_t n) {
+    if (p + 4 <= n) return ld32(s + p);
+    uint32_t x = 0;
+    for (int k = 0; k < 3; ++k)
+        if (p + k < n) x |= (uint32_t)s[p + k] << (8 * k);
+    return x;
+}
+
+// Candidates of one 64-position chunk; the verify loads are issued here and
+// consumed by chunk_finish, so their latency overlaps the previous chunk's
+// parse and encode.
+struct Chunk {
+    uint32_t v;       // bytes [p, p + 4) of this lane's position
+    int32_t cand;     // candidate position or -1
+    bool okc;         // candidate worth verifying
+    uint32_t xc;      // bytes at cand
+    u32x4 fa, fc;     // 16 bytes after p / after cand
+    uint32_t bp, bc;  // 4 bytes before p / before cand
+};
+
+template <bool BIG>
+__device__ __forceinline__ void chunk_issue(Chunk& C, const uint8_t* s, uint32_t* table32, int32_t p0, uint32_t v,
+                                            int32_t N, int32_t mlast, uint32_t lane) {
+    const int32_t p = p0 + (int32_t)lane;
+    const bool act = p + 4 <= N;
+    const uint32_t h = act ? phash(v) : 8192u;
+    // nearest earlier / later lane with the same hash: bitonic sort of (hash, lane)
+    const uint32_t key = wave_sort((h << 6) | lane, lane);
+    const uint32_t kprev = (uint32_t)__builtin_amdgcn_update_dpp((int)key, (int)key, 0x138, 0xF, 0xF, false);
+    const uint32_t knext = (uint32_t)__builtin_amdgcn_update_dpp((int)key, (int)key, 0x130, 0xF, 0xF, false);
+    const bool sprev = lane > 0 && (kprev >> 6) == (key >> 6);
+    const bool snext = lane < 63 && (knext >> 6) == (key >> 6);
+    const uint32_t info = (sprev ? (0x40u | (kprev & 63)) : 0u) | (snext ? 0x80u : 0u);
+    const uint32_t mine = (uint32_t)__builtin_amdgcn_ds_permute((int)((key & 63) << 2), (int)info);
+    uint16_t* table16 = reinterpret_cast<uint16_t*>(table32);
+    const uint32_t empty = BIG ? 0xFFFFFFFFu : kEmpty;
+    const uint32_t old = act ? (BIG ? table32[h] : (uint32_t)table16[h]) : empty;
+    const int32_t cand = (mine & 0x40u) ? p0 + (int32_t)(mine & 63) : (old == empty ? -1 : (int32_t)old);
+    if (act && !(mine & 0x80u)) {
+        if (BIG) {
+            table32[h] = (uint32_t)p;
+        } else {
+            table16[h] = (uint16_t)p;
+        }
+    }
+    C.v = v;
+    C.cand = cand;
+    // LZ4_DISTANCE_MAX (lz4.c:1064): only checkable past 64 KiB
+    C.okc = act && cand >= 0 && p <= mlast && (!BIG || p - cand <= 65535);
+    // every address stays inside the block (N >= 4 here; p <= mlast when okc)
+    const int32_t cs = C.okc ? cand : 0;
+    const int32_t ps = C.okc ? p : 0;
+    C.xc = ld32(s + cs);
+    C.fa = ld16_guarded(s + ps + 4, N - ps - 4);
+    C.fc = ld16_guarded(s + cs + 4, N - cs - 4);
+    const bool bk = C.okc && cand >= 4;
+    C.bp = bk ? ld32(s + p - 4) : 0u;
+    C.bc = bk ? ld32(s + cand - 4) : 1u;
+}
+
+__device__ __forceinline__ uint64_t chunk_finish(const Chunk& C, int32_t p0, int32_t matchlimit, int32_t& L,
+                                                 int32_t& back, uint32_t lane) {
+    const int32_t p = p0 + (int32_t)lane;
+    const int32_t lim = matchlimit - p;
+    const bool ok = C.okc && C.xc == C.v && lim >= 4;
+    L = 4 + (int32_t)eq_prefix16(C.fa, C.fc);
+    if (L > lim) L = lim;
+    const uint32_t x = C.bp ^ C.bc;
+    back = C.cand >= 4 ? (x ? (int32_t)(__builtin_clz(x) >> 3) : 4) : 0;
+    return __ballot(ok);
+}
+
+template <bool BIG>
 __global__ __launch_bounds__(64) void pcompress_kernel(const uint8_t* __restrict__ src,
                                                        const int64_t* __restrict__ src_off,
                                                        const int32_t* __restrict__ src_len, uint8_t* __restrict__ dst,
                                                        const int64_t* __restrict__ dst_off,
                                                        const int32_t* __restrict__ dst_cap,
                                                        int32_t* __restrict__ out_len, int64_t n) {
-    __shared__ __attribute__((aligned(16))) uint16_t table[8192];
+    // 8192 hash4 entries: u16 positions (blocks <= 64 KiB) or u32 (BIG)
+    __shared__ __attribute__((aligned(16))) uint32_t table[BIG ? 8192 : 4096];
     const uint32_t lane = threadIdx.x;
     for (int64_t b = blockIdx.x; b < n; b += gridDim.x) {
         const int32_t N = src_len[b];
         const int32_t cap = dst_cap[b];
         const uint8_t* s = src + src_off[b];
         uint8_t* d = dst + dst_off[b];
-        if (N < 0 || N > 65536) {   // this kernel handles blocks up to 64 KiB
+        if (N < 0 || (!BIG && N > 65536)) {   // the u16 table covers blocks up to 64 KiB
             if (lane == 0) out_len[b] = 0;
             continue;
         }
-        for (int k = (int)lane; k < 8192 / 8; k += 64)
+        for (int k = (int)lane; k < (BIG ? 8192 : 4096) / 4; k += 64)
             reinterpret_cast<u32x4*>(table)[k] = u32x4{0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
         int32_t anchor = 0, cur = 0, op = 0;
         bool fail = false;
         const int32_t mlast = N - 12;      // last match start (MFLIMIT)
         const int32_t matchlimit = N - 5;  // match end bound (LASTLITERALS)
+        uint32_t vprev = 0;
+        Chunk A;
+        int32_t L = 0, back = 0;
+        uint64_t mask = 0;
+        if (N >= 4) {
+            chunk_issue<BIG>(A, s, table, 0, load_word(s, (int32_t)lane, N), N, mlast, lane);
+            mask = chunk_finish(A, 0, matchlimit, L, back, lane);
+        }
         for (int32_t p0 = 0; p0 + 4 <= N; p0 += 64) {
-            const int32_t p = p0 + (int32_t)lane;
-            const bool act = p + 4 <= N;
-            const uint32_t v = act ? ld32(s + p) : 0u;
-            const uint32_t h = act ? phash(v) : 8192u;
-            // ---- nearest earlier / later lane with the same hash: bitonic sort
-            uint32_t key = (h << 6) | lane;
-#pragma unroll
-            for (int k = 2; k <= 64; k <<= 1) {
-#pragma unroll
-                for (int j = k >> 1; j > 0; j >>= 1) {
-                    const uint32_t other = (uint32_t)__shfl_xor((int)key, j);
-                    const bool up = (lane & k) == 0;
-                    const bool lower = (lane & j) == 0;
-                    key = (lower == up) ? (key < other ? key : other) : (key > other ? key : other);
-                }
-            }
-            const uint32_t kprev = (uint32_t)__shfl_up((int)key, 1);
-            const uint32_t knext = (uint32_t)__shfl_down((int)key, 1);
-            const bool sprev = lane > 0 && (kprev >> 6) == (key >> 6);
-            const bool snext = lane < 63 && (knext >> 6) == (key >> 6);
-            const uint32_t info = (sprev ? (0x40u | (kprev & 63)) : 0u) | (snext ? 0x80u : 0u);
-            // deliver to the original lane (key & 63)
-            const uint32_t mine = (uint32_t)__builtin_amdgcn_ds_permute((int)((key & 63) << 2), (int)info);
-            // ---- table
-            const uint32_t old = act ? table[h] : kEmpty;
-            int32_t cand = (mine & 0x40u) ? p0 + (int32_t)(mine & 63) : (old == kEmpty ? -1 : (int32_t)old);
-            if (act && !(mine & 0x80u)) table[h] = (uint16_t)p;
-            // ---- verify + forward / backward lengths
-            bool ok = act && cand >= 0 && p <= mlast;
-            int32_t L = 0, back = 0;
-            if (ok) ok = ld32(s + cand) == v;
-            if (ok) {
-                const int32_t lim = matchlimit - p;   // max match length here
-                if (lim < 4) {
-                    ok = false;
-                } else {
-                    const u32x4 a = ld16_guarded(s + p + 4, N - p - 4);
-                    const u32x4 c = ld16_guarded(s + cand + 4, N - cand - 4);
-                    L = 4 + (int32_t)eq_prefix16(a, c);
-                    if (L > lim) L = lim;
-                    if (cand >= 4) {
-                        const uint32_t x = ld32(s + p - 4) ^ ld32(s + cand - 4);
-                        back = x ? (int32_t)(__builtin_clz(x) >> 3) : 4;
-                    }
-                }
-            }
-            const uint64_t mask = __ballot(ok);
-            // ---- greedy parse of this step's positions
+            const bool has_next = p0 + 68 <= N;
+            Chunk B;
+            if (has_next)
+                chunk_issue<BIG>(B, s, table, p0 + 64, load_word(s, p0 + 64 + (int32_t)lane, N), N, mlast, lane);
+            // ---- greedy parse of chunk p0
             int ns = 0;
-            int32_t q_ls = 0, q_lit = 0, q_off = 0, q_ml = 0;   // sequence ns lives in lane ns
+            int32_t q_ls = 0, q_lit = 0, q_off = 0, q_ml = 0, q_ob = 0, q_pb = 0;   // sequence ns in lane ns
+            int32_t acc = 0, pacc = 0;
             while (cur < p0 + 64 && cur <= mlast) {
                 const int32_t rel = cur - p0;
-                const uint64_t m = rel <= 0 ? mask : (rel >= 64 ? 0ull : (mask >> rel) << rel);
+                const uint64_t m = rel <= 0 ? mask : (mask >> rel) << rel;
                 if (m == 0) break;
                 const int j = __builtin_ctzll(m);
                 int32_t st = p0 + j;
-                int32_t c = rdl(cand, j);
+                int32_t c = rdl(A.cand, j);
                 int32_t len = rdl(L, j);
                 int32_t bk = rdl(back, j);
                 const int32_t lim = matchlimit - st;
@@ -218,28 +341,42 @@ __global__ __launch_bounds__(64) void pcompress_kernel(const uint8_t* __restrict
                 st -= bk;
                 c -= bk;
                 len += bk;
+                const int32_t lit = st - anchor;
                 if ((int)lane == ns) {
                     q_ls = anchor;
-                    q_lit = st - anchor;
+                    q_lit = lit;
                     q_off = st - c;
                     q_ml = len;
+                    q_ob = acc;
+                    q_pb = pacc;
                 }
+                const int32_t sz = seq_size(lit, len);
+                acc += sz;
+                pacc += lit >= kLongLit ? sz - lit : sz;
                 ++ns;
                 cur = st + len;
                 anchor = cur;
                 if (ns == 64) break;
             }
             if (ns > 0) {
-                const int32_t w = emit_seqs(s, d, op, cap, ns, q_ls, q_lit, q_off, q_ml, lane);
+                const int32_t w = emit_seqs(s, d, op, cap, ns, q_ls, q_lit, q_off, q_ml, q_ob, q_pb, acc, pacc, p0,
+                                            A.v, vprev, lane);
                 if (w < 0) {
                     fail = true;
                     break;
                 }
                 op += w;
             }
+            if (!has_next) break;
+            vprev = A.v;
+            A = B;
+            mask = chunk_finish(A, p0 + 64, matchlimit, L, back, lane);
         }
         if (!fail) {   // last literals (lz4.c:1266-1293)
-            const int32_t w = emit_seqs(s, d, op, cap, 1, anchor, N - anchor, 0, 0, lane);
+            const int32_t lit = N - anchor;
+            const int32_t sz = seq_size(lit, 0);
+            const int32_t w = emit_seqs(s, d, op, cap, 1, anchor, lit, 0, 0, 0, 0, sz,
+                                        lit >= kLongLit ? sz - lit : sz, 1 << 30, 0u, 0u, lane);
             if (w < 0) {
                 fail = true;
             } else {
@@ -251,11 +388,16 @@ __global__ __launch_bounds__(64) void pcompress_kernel(const uint8_t* __restrict
 }
 
 int pcompress_launch(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len, uint8_t* d_dst,
-                     const int64_t* d_dst_off, const int32_t* d_dst_cap, int32_t* d_out_len, int64_t n,
+                     const int64_t* d_dst_off, const int32_t* d_dst_cap, int32_t* d_out_len, int64_t n, bool big,
                      hipStream_t stream) {
     const uint32_t grid = (uint32_t)(n < (1ll << 30) ? n : (1ll << 30));
-    hipLaunchKernelGGL(pcompress_kernel, dim3(grid), dim3(64), 0, stream, d_src, d_src_off, d_src_len, d_dst,
-                       d_dst_off, d_dst_cap, d_out_len, n);
+    if (big) {
+        hipLaunchKernelGGL(pcompress_kernel<true>, dim3(grid), dim3(64), 0, stream, d_src, d_src_off, d_src_len,
+                           d_dst, d_dst_off, d_dst_cap, d_out_len, n);
+    } else {
+        hipLaunchKernelGGL(pcompress_kernel<false>, dim3(grid), dim3(64), 0, stream, d_src, d_src_off, d_src_len,
+                           d_dst, d_dst_off, d_dst_cap, d_out_len, n);
+    }
     return (int)hipGetLastError();
 }
 

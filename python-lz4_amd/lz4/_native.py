@@ -22,6 +22,7 @@ TABLE_U16_HASH4 = 0
 TABLE_U32_HASH5 = 1
 TABLE_AUTO = 2
 PARSE_PARALLEL = 3   # parallel-parse compressor: valid blocks, ratio of LZ4_compress_default
+PARSE_PARALLEL_LARGE = 4   # the same for blocks > 64 KiB
 EINVAL = 0x10000
 
 _lock = threading.Lock()

@@ -150,11 +150,33 @@ def compress(data, compression_level=0, block_size=0, content_checksum=False, bl
     src = _buffer(data, "data")
     level = _c_int(compression_level, "compression_level")
     bsid_req = _c_int(block_size, "block_size")
+    dev = N.device()
+    d_src = N.to_device(src, dev, pad=1)
+    frame = compress_device(d_src, src.nbytes, compression_level=level, block_size=bsid_req,
+                            content_checksum=content_checksum, block_checksum=block_checksum,
+                            block_linked=block_linked, store_size=store_size)
+    out = frame.cpu().numpy().tobytes()
+    return bytearray(out) if return_bytearray else out
+
+
+def compress_device(d_src: torch.Tensor, n: int | None = None, *, compression_level=0, block_size=0,
+                    content_checksum=False, block_checksum=False, block_linked=True, store_size=True,
+                    parse="exact", stream=None) -> torch.Tensor:
+    """Device-resident LZ4F_compressFrame: the frame of d_src[:n] as a uint8
+    device tensor (no host round trip).
+
+    parse="exact": blocks byte-identical to LZ4_compress_default, i.e. the
+    frame is byte-identical to the reference's for independent blocks.
+    parse="parallel": the parallel-parse compressor (valid blocks at the
+    ratio of LZ4_compress_default, not byte-identical; BASELINE config 4)."""
+    n = d_src.numel() if n is None else int(n)
+    level = int(compression_level)
     if level >= 3:
         raise NotImplementedError("LZ4 HC compression levels (>= 3) are outside the MI355X codec's scope")
+    if parse not in ("exact", "parallel"):
+        raise ValueError("parse must be 'exact' or 'parallel'")
     accel = -level + 1 if level < 0 else 1                     # lz4frame.c:855
-    n = src.nbytes
-    bsid = _optimal_bsid(bsid_req, n)
+    bsid = _optimal_bsid(int(block_size), n)
     if bsid == 0:
         bsid = BLOCKSIZE_MAX64KB                               # LZ4F_BLOCKSIZEID_DEFAULT
     if bsid not in _BLOCK_SIZES:
@@ -163,11 +185,10 @@ def compress(data, compression_level=0, block_size=0, content_checksum=False, bl
     linked = bool(block_linked) and n > bsize                  # lz4frame.c:441-442
     content_size = n if store_size else 0
     hdr = _header(bsid, linked, bool(block_checksum), content_size, bool(content_checksum))
-
-    dev = N.device()
-    d_src = N.to_device(src, dev, pad=1)
+    dev = d_src.device
     nb = (n + bsize - 1) // bsize
-    parts = [hdr]
+    total = 0
+    body = None
     if nb:
         raw_off = torch.arange(nb, dtype=torch.int64, device=dev) * bsize
         raw_len = torch.full((nb,), bsize, dtype=torch.int32, device=dev)
@@ -177,19 +198,29 @@ def compress(data, compression_level=0, block_size=0, content_checksum=False, bl
         cmp = torch.empty(nb * slot, dtype=torch.uint8, device=dev)
         cmp_off = torch.arange(nb, dtype=torch.int64, device=dev) * slot
         cmp_len = torch.empty(nb, dtype=torch.int32, device=dev)
-        N.launch_compress(d_src, raw_off, raw_len, cmp, cmp_off, cap, cmp_len, nb, N.TABLE_AUTO, accel)
+        if parse == "exact":
+            table = N.TABLE_AUTO
+        else:
+            table = N.PARSE_PARALLEL if bsize <= 65536 else N.PARSE_PARALLEL_LARGE
+        N.launch_compress(d_src, raw_off, raw_len, cmp, cmp_off, cap, cmp_len, nb, table, accel, stream)
         rec_len = torch.empty(nb, dtype=torch.int32, device=dev)
-        N.frame_block_sizes(raw_len, cmp_len, block_checksum, rec_len, nb)
-        frame_off = N.exclusive_scan(rec_len)
+        N.frame_block_sizes(raw_len, cmp_len, block_checksum, rec_len, nb, stream)
+        frame_off = N.exclusive_scan(rec_len, stream=stream)
         total = int(frame_off[-1].item())
-        body = torch.empty(total + 16, dtype=torch.uint8, device=dev)
-        N.frame_emit(d_src, raw_off, raw_len, cmp, cmp_off, cmp_len, body, frame_off, block_checksum, nb)
-        parts.append(body[:total].cpu().numpy().tobytes())
-    parts.append(b"\x00\x00\x00\x00")                          # endmark, lz4frame.c:1167
-    if content_checksum:
-        parts.append(struct.pack("<I", _xxh32_dev(d_src, n)))  # lz4frame.c:1170-1176
-    out = b"".join(parts)
-    return bytearray(out) if return_bytearray else out
+    tail = 4 + (4 if content_checksum else 0)
+    out = torch.empty(len(hdr) + total + tail + 16, dtype=torch.uint8, device=dev)
+    out[: len(hdr)] = torch.frombuffer(bytearray(hdr), dtype=torch.uint8).to(dev)
+    if nb:
+        body = out[len(hdr):]
+        N.frame_emit(d_src, raw_off, raw_len, cmp, cmp_off, cmp_len, body, frame_off, block_checksum, nb, stream)
+        del cmp
+    pos = len(hdr) + total
+    out[pos: pos + 4] = 0                                      # endmark, lz4frame.c:1167
+    if content_checksum:                                       # lz4frame.c:1170-1176
+        h = torch.empty(1, dtype=torch.int32, device=dev)
+        N.launch_xxh32_long(d_src, n, 0, h, stream)
+        out[pos + 4: pos + 8] = h.view(torch.uint8)
+    return out[: pos + tail]
 
 
 # -------------------------------------------------------------- decompress

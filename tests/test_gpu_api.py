@@ -224,6 +224,27 @@ def test_reference_decodes_our_frames(gpu, reference):
             assert code == 0 and out == data
 
 
+@pytest.mark.parametrize("parse", ["exact", "parallel"])
+def test_frame_compress_device(gpu, reference, parse):
+    """Device-resident frame compress (config 4 path): decodes with the
+    reference LZ4F_decompress and with lz4.frame.decompress; the exact parse
+    equals lz4.frame.compress byte for byte."""
+    import torch
+    import oracle as O
+    from lz4 import _synth
+    data = _synth.blocks(80, "silesia", seed=9).tobytes()[:5_000_000]
+    d = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(gpu)
+    for bs in (lz4.frame.BLOCKSIZE_MAX64KB, lz4.frame.BLOCKSIZE_MAX4MB):
+        f = lz4.frame.compress_device(d, block_size=bs, block_linked=False, content_checksum=True,
+                                      block_checksum=(bs == 4), parse=parse).cpu().numpy().tobytes()
+        code, out = O.ref_decompress_frame(reference, f)
+        assert code == 0 and out == data, (parse, bs)
+        assert lz4.frame.decompress(f) == data
+        if parse == "exact":
+            assert f == lz4.frame.compress(data, block_size=bs, block_linked=False, content_checksum=True,
+                                           block_checksum=(bs == 4))
+
+
 def test_frame_truncated(gpu):
     data = os.urandom(256 * 1024)
     c = lz4.frame.compress(data)
