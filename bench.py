@@ -146,6 +146,8 @@ def main():
     ap.add_argument("--random-blocks", type=int, default=1 << 17, help="blocks of the random-data extra line")
     ap.add_argument("--gather-blocks", type=int, default=1 << 16,
                     help="N>1: compressed blocks per rank gathered at rank 0 over RCCL (config 5 exchange)")
+    ap.add_argument("--frame-gib", type=int, default=8,
+                    help="config 4: GiB of input in one LZ4 frame of 4 MiB independent blocks + content checksum; 0 = skip")
     ap.add_argument("--e2e-blocks", type=int, default=1 << 15,
                     help="blocks of the host-to-host (PCIe-inclusive) extra line; 0 = skip")
     args = ap.parse_args()
@@ -165,20 +167,42 @@ def main():
     src = make_batch(n, args.pool, "silesia", seed=2026 + rank, dev=dev)
     log(f"[bench] data ready in {time.perf_counter() - t_gen:.1f}s")
 
-    # ---- compress (config 3): LZ4_compress_default parse (byU16/hash4) ----
-    src_off, src_len, slots, slot_off, slot_cap, out_len = compress_all(src, n, N.TABLE_U16_HASH4, dev)
+    # ---- compress (config 3): parallel-parse compressor, ratio vs LZ4_compress_default ----
+    src_off, src_len, slots, slot_off, slot_cap, out_len = compress_all(src, n, N.PARSE_PARALLEL, dev)
+    dst = torch.empty(n * BLOCK, dtype=torch.uint8, device=dev)
+    dst_off = torch.arange(n, dtype=torch.int64, device=dev) * BLOCK
+    dst_cap = torch.full((n,), BLOCK, dtype=torch.int32, device=dev)
+    status = torch.empty(n, dtype=torch.int32, device=dev)
 
-    def do_compress():
+    def do_pcompress():
+        N.launch_compress(src, src_off, src_len, slots, slot_off, slot_cap, out_len, n, N.PARSE_PARALLEL, 1)
+
+    c3 = {}
+    if not args.no_compress:
+        c_wall, c_ev = time_kernel(do_pcompress, max(1, args.steps // 2), 1, world)
+        assert int((out_len <= 0).sum()) == 0, "parallel compress failed on some block"
+        par_total = int(out_len.to(torch.int64).sum())
+        # validity at full size: our decoder (bit-exact to LZ4_decompress_safe)
+        # must restore every block
+        N.launch_decompress(slots, slot_off, out_len, dst, dst_off, dst_cap, status, n)
+        assert bool((status == BLOCK).all()) and torch.equal(dst, src), "parallel-parse blocks do not round-trip"
+        c3 = {"compress_gib_s": round(world * n * BLOCK / (c_wall / max(1, args.steps // 2)) / GIB, 2),
+              "compress_kernel_ms": round(c_ev * 1e3, 3),
+              "compress_ratio": round(n * BLOCK / par_total, 4),
+              "compress_algo_gbs": round((n * BLOCK + par_total) / c_ev / 1e9, 1)}
+
+    log("[bench] parallel compress done")
+    # ---- decode input: the exact LZ4_compress_default parse (byU16/hash4) ----
+    def do_compress_exact():
         N.launch_compress(src, src_off, src_len, slots, slot_off, slot_cap, out_len, n, N.TABLE_U16_HASH4, 1)
 
-    if args.no_compress:
-        do_compress()
-        c_wall, c_ev = float("nan"), float("nan")
-    else:
-        c_wall, c_ev = time_kernel(do_compress, max(1, args.steps // 2), 1, world)
+    x_wall, x_ev = time_kernel(do_compress_exact, 1, 0, world)
     assert int((out_len <= 0).sum()) == 0, "compress failed on some block"
     comp_total = int(out_len.to(torch.int64).sum())
     ratio = n * BLOCK / comp_total
+    if c3:
+        c3["compress_ratio_vs_default"] = round(c3["compress_ratio"] / ratio, 4)
+    c3["compress_exact_gib_s"] = round(world * n * BLOCK / x_wall / GIB, 2)
 
     # compact into one contiguous compressed buffer (what a file/socket holds)
     offs = N.exclusive_scan(out_len)
@@ -195,12 +219,8 @@ def main():
     del slots, slot_off, slot_cap
     torch.cuda.empty_cache()
 
+    log("[bench] exact compress done")
     # ---- decompress (config 2, headline) ----
-    dst = torch.empty(n * BLOCK, dtype=torch.uint8, device=dev)
-    dst_off = torch.arange(n, dtype=torch.int64, device=dev) * BLOCK
-    dst_cap = torch.full((n,), BLOCK, dtype=torch.int32, device=dev)
-    status = torch.empty(n, dtype=torch.int32, device=dev)
-
     def do_decompress():
         N.launch_decompress(comp, c_off, c_len, dst, dst_off, dst_cap, status, n)
 
@@ -273,6 +293,55 @@ def main():
         r_cbytes = int(r_olen.to(torch.int64).sum())
         extra["decompress_random_gib_s"] = round(world * nr * BLOCK / (r_wall / args.steps) / GIB, 2)
         extra["decompress_random_kernel_gbs"] = round((r_cbytes + nr * BLOCK) / r_ev / 1e9, 1)
+        del rsrc, rdst, r_slots, rst
+
+    log("[bench] decode done")
+    # ---- extra: config 4, one frame of 4 MiB independent blocks + XXH32 content checksum ----
+    if args.frame_gib > 0:
+        from lz4.frame._frame import _compress_frame
+        dst = dst_off = dst_cap = None
+        torch.cuda.empty_cache()
+        FB = 4 << 20
+        L = args.frame_gib << 30
+        fsrc = make_batch(L // BLOCK, min(args.pool, L // BLOCK), "silesia", seed=77 + rank, dev=dev)
+        kw = dict(block_size=7, block_linked=False, parse="parallel")
+        box = {}
+
+        def do_frame():
+            box["f"] = _compress_frame(fsrc, L, content_checksum=True, **kw)
+
+        def do_frame_nochk():
+            box["g"] = _compress_frame(fsrc, L, content_checksum=False, **kw)
+
+        hsum = torch.empty(1, dtype=torch.int32, device=dev)
+        f_wall, _ = time_kernel(do_frame, 1, 1, world)
+        g_wall, _ = time_kernel(do_frame_nochk, 1, 0, world)
+        h_wall, h_ev = time_kernel(lambda: N.launch_xxh32_long(fsrc, L, 0, hsum), 1, 0, world)
+        frame, meta = box.pop("f")
+        box.clear()
+        # validate: decode every block of the frame on the device, check the
+        # content checksum field and the round trip
+        nbk = L // FB
+        assert not bool(meta["raw"].any()), "unexpected stored-raw block"
+        fdst = torch.empty(L, dtype=torch.uint8, device=dev)
+        fst = torch.empty(nbk, dtype=torch.int32, device=dev)
+        t0 = time.perf_counter()
+        N.launch_decompress(frame, meta["data_off"], meta["stored_len"], fdst,
+                            torch.arange(nbk, dtype=torch.int64, device=dev) * FB,
+                            torch.full((nbk,), FB, dtype=torch.int32, device=dev), fst, nbk)
+        torch.cuda.synchronize()
+        fd_s = time.perf_counter() - t0
+        assert bool((fst == FB).all()) and torch.equal(fdst, fsrc), "config-4 frame does not round-trip"
+        assert int(frame[-4:].view(torch.int32).item()) == int(hsum.item()), "content checksum field mismatch"
+        extra["frame4m"] = {
+            "input_gib": args.frame_gib, "blocks": nbk, "ratio": round(L / frame.numel(), 4),
+            "compress_frame_gib_s": round(world * L / f_wall / GIB, 2),
+            "compress_frame_no_content_checksum_gib_s": round(world * L / g_wall / GIB, 2),
+            "content_xxh32_gb_s": round(L / h_ev / 1e9, 3),
+            "decode_blocks_gib_s": round(world * L / fd_s / GIB, 2),
+            "note": "content XXH32 is one serial stream (SURVEY 0.5); it runs beside the block compression"}
+        del fsrc, fdst, frame, meta
+        torch.cuda.empty_cache()
 
     # ---- report ----
     d_step = d_wall / args.steps
@@ -310,9 +379,8 @@ def main():
                    "parallelism": f"shard{world}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic},
-        "compress_gib_s": None if c_wall != c_wall else round(world * n * BLOCK / (c_wall / max(1, args.steps // 2)) / GIB, 2),
-        "compress_kernel_ms": None if c_ev != c_ev else round(c_ev * 1e3, 3),
         "decompress_kernel_ms": round(d_ev * 1e3, 3),
+        "compress": c3,
         "extra": extra,
     }
     if comp_sample is not None:

@@ -168,7 +168,21 @@ def compress_device(d_src: torch.Tensor, n: int | None = None, *, compression_le
     parse="exact": blocks byte-identical to LZ4_compress_default, i.e. the
     frame is byte-identical to the reference's for independent blocks.
     parse="parallel": the parallel-parse compressor (valid blocks at the
-    ratio of LZ4_compress_default, not byte-identical; BASELINE config 4)."""
+    ratio of LZ4_compress_default, not byte-identical; BASELINE config 4).
+
+    The content checksum (one serial XXH32 stream over all of d_src) runs on
+    its own stream beside the block compression."""
+    return _compress_frame(d_src, n, compression_level=compression_level, block_size=block_size,
+                           content_checksum=content_checksum, block_checksum=block_checksum,
+                           block_linked=block_linked, store_size=store_size, parse=parse, stream=stream)[0]
+
+
+def _compress_frame(d_src, n=None, *, compression_level=0, block_size=0, content_checksum=False,
+                    block_checksum=False, block_linked=True, store_size=True, parse="exact", stream=None):
+    """compress_device, also returning the block records:
+    (frame, {"data_off", "stored_len", "raw"}) with device tensors giving, per
+    block, the payload position in the frame, its stored length and whether
+    it is stored raw (None when the input is empty)."""
     n = d_src.numel() if n is None else int(n)
     level = int(compression_level)
     if level >= 3:
@@ -189,6 +203,15 @@ def compress_device(d_src: torch.Tensor, n: int | None = None, *, compression_le
     nb = (n + bsize - 1) // bsize
     total = 0
     body = None
+    meta = None
+    main = stream if stream is not None else torch.cuda.current_stream(dev)
+    h = None
+    if content_checksum:                                       # lz4frame.c:1042, 1170-1176
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(main)
+        h = torch.empty(1, dtype=torch.int32, device=dev)
+        N.launch_xxh32_long(d_src, n, 0, h, side)
+        h.record_stream(main)
     if nb:
         raw_off = torch.arange(nb, dtype=torch.int64, device=dev) * bsize
         raw_len = torch.full((nb,), bsize, dtype=torch.int32, device=dev)
@@ -214,13 +237,15 @@ def compress_device(d_src: torch.Tensor, n: int | None = None, *, compression_le
         body = out[len(hdr):]
         N.frame_emit(d_src, raw_off, raw_len, cmp, cmp_off, cmp_len, body, frame_off, block_checksum, nb, stream)
         del cmp
+        stored = rec_len - 4 - (4 if block_checksum else 0)
+        meta = {"data_off": frame_off[:nb] + len(hdr) + 4, "stored_len": stored,
+                "raw": (cmp_len <= 0) | (cmp_len >= raw_len)}
     pos = len(hdr) + total
     out[pos: pos + 4] = 0                                      # endmark, lz4frame.c:1167
-    if content_checksum:                                       # lz4frame.c:1170-1176
-        h = torch.empty(1, dtype=torch.int32, device=dev)
-        N.launch_xxh32_long(d_src, n, 0, h, stream)
+    if content_checksum:
+        main.wait_stream(side)
         out[pos + 4: pos + 8] = h.view(torch.uint8)
-    return out[: pos + tail]
+    return out[: pos + tail], meta
 
 
 # -------------------------------------------------------------- decompress

@@ -197,14 +197,19 @@ def test_xxh32_batch(gpu, oracle, corpus):
         assert got == [oracle.xxh32(b, seed) for b in items]
 
 
-@pytest.mark.parametrize("n", [0, 1, 15, 16, 17, 1023, 1024, 1025, 4096 + 7, 3 * 65536 + 5])
-def test_xxh32_long(gpu, oracle, corpus, n):
+@pytest.mark.parametrize("n", [0, 1, 15, 16, 17, 63, 64, 511, 512, 513, 1023, 1024, 1025, 4096 + 7,
+                               3 * 65536 + 5, (1 << 20) + 77])
+@pytest.mark.parametrize("shift", [0, 1, 3, 4])
+def test_xxh32_long(gpu, oracle, corpus, n, shift):
+    """Content-checksum kernel (scalar-loaded path for dword-aligned sources,
+    vector path otherwise) against the oracle's XXH32, several seeds."""
     blocks, _ = corpus
-    data = (b"".join(blocks[:4]))[:n]
-    d = N.to_device(data, gpu, pad=1)
+    data = (b"".join(blocks) * 2)[:n]
+    d = N.to_device(b"\x00" * shift + data, gpu, pad=1)[shift:]
     out = torch.empty(1, dtype=torch.int32, device=gpu)
-    N.launch_xxh32_long(d, n, 0, out)
-    assert out.item() & 0xFFFFFFFF == oracle.xxh32(data)
+    for seed in (0, 0x9E3779B1):
+        N.launch_xxh32_long(d, n, seed, out)
+        assert out.item() & 0xFFFFFFFF == oracle.xxh32(data, seed)
 
 
 def test_scan_and_gather(gpu):
