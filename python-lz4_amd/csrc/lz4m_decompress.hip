@@ -60,7 +60,7 @@ struct Lane {
 };
 
 // ------------------------------------------------------ LDS staging (hot kernel)
-// Output is assembled in a per-lane LDS stage and leaves for HBM in whole,
+// Output is assembled in a per-lane 96-byte LDS stage and leaves for HBM in whole,
 // contiguous 64-byte chunks (4 x 16-byte stores by one lane): every HBM line
 // is written once, instead of piecemeal by 1-16 byte stores from thousands of
 // interleaved lane streams.  The token stream is read through a per-lane
@@ -71,15 +71,22 @@ struct Lane {
 // ds_read/ds_write_b128 without wrap-around logic; stores into the stage are
 // wild 16-byte stores (like the reference's wild copies) and only the final
 // partial chunk is written to HBM byte-exactly.
-constexpr int kStage = 128;
+// The stage holds output [F - 16, F + 80): stores at p < F + 64 (16 bytes,
+// wild) stay inside, and [F - 16, F) keeps the bytes a short match may
+// still read.  96 + 64 bytes per lane is 40 KB per 256-lane workgroup, so 4
+// workgroups (16 waves) fit a CU's 160 KB of LDS -- the decoder is latency
+// bound, and 16 waves/CU decode 1.15-1.3x faster than 12 with 128-byte
+// stages (tools/prof_decode.py, MI355X).
+constexpr int kStage = 96;
 constexpr int kWin = 64;
 
 __device__ __forceinline__ uint8_t* stage_at(const Lane& L, int64_t p) { return L.stage + (p - L.F + 16); }
 
-// Chunk [F, F + 64) is final: write it to HBM and rebase the stage by 64.
+// Chunk [F, F + 64) is final: write it to HBM and rebase the stage by 64
+// (the 32 bytes [F + 48, F + 80) move to the front).
 __device__ __forceinline__ void stage_flush(Lane& L) {
     const u32x4 a = ld16(L.stage + 16), b = ld16(L.stage + 32), c = ld16(L.stage + 48), d = ld16(L.stage + 64);
-    const u32x4 e = ld16(L.stage + 80), f = ld16(L.stage + 96), g = ld16(L.stage + 112);
+    const u32x4 e = ld16(L.stage + 80);
     uint8_t* o = L.dst + L.F;
     st16(o, a);
     st16(o + 16, b);
@@ -87,8 +94,6 @@ __device__ __forceinline__ void stage_flush(Lane& L) {
     st16(o + 48, d);
     st16(L.stage, d);
     st16(L.stage + 16, e);
-    st16(L.stage + 32, f);
-    st16(L.stage + 48, g);
     L.F += 64;
 }
 
@@ -129,11 +134,41 @@ __device__ __forceinline__ void put_exact(uint8_t* p, u32x4 v, uint32_t k) {
     if (k & 1) p[o] = (uint8_t)window_dword(v, o);
 }
 
+// ------------------------------------------------ input reads (general path)
+// The general state machine reads the compressed block byte by byte (length
+// bytes, offsets) and in 16-byte pieces (token window, literals).  In STAGE
+// mode these come from the lane's LDS input window [ib, ib + 64) when they
+// lie inside it (it holds the block's bytes, zeros past iend -- the same
+// values ld16_guarded returns), else from HBM: a general step then costs LDS
+// latencies instead of a chain of dependent HBM round trips.
+template <bool STAGE>
+__device__ __forceinline__ uint32_t in_byte(const Lane& L, int64_t p) {
+    if (STAGE) {
+        const int64_t d = p - L.ib;
+        if (d >= 0 && d < kWin) return L.win[d];
+    }
+    return L.src[p];
+}
+
+template <bool STAGE>
+__device__ __forceinline__ u32x4 in16(const Lane& L, int64_t p) {
+    if (STAGE) {
+        const int64_t d = p - L.ib;
+        if (d >= 0 && d <= kWin - 16) return ld16(L.win + d);
+    }
+    return ld16_guarded(L.src + p, L.iend - p);
+}
+
+template <bool STAGE>
+__device__ __forceinline__ uint32_t in_le16(const Lane& L, int64_t p) {
+    return in_byte<STAGE>(L, p) | (in_byte<STAGE>(L, p + 1) << 8);
+}
+
 // Literal of len <= 64 bytes read from the compressed block.
 __device__ __forceinline__ void stage_literal(Lane& L, int64_t op, int64_t ip, int64_t len) {
     for (int64_t i = 0; i < len; i += 16) {
         stage_sync(L, op + i);
-        st16(stage_at(L, op + i), ld16_guarded(L.src + ip + i, L.iend - ip - i));
+        st16(stage_at(L, op + i), in16<true>(L, ip + i));
     }
 }
 
@@ -317,13 +352,14 @@ __device__ __forceinline__ void wave_match(uint8_t* d, int64_t off, int64_t len,
 // ------------------------------------------------------------ lane decode
 // read_variable_length (lz4.c:1903-1928).  On failure *ip is the position
 // the reference reports.
-__device__ __forceinline__ bool read_len(const uint8_t* src, int64_t& ip, int64_t ilimit, bool initial_check,
+template <bool STAGE>
+__device__ __forceinline__ bool read_len(const Lane& L, int64_t& ip, int64_t ilimit, bool initial_check,
                                          int64_t& out) {
     if (initial_check && ip >= ilimit) return false;
     int64_t len = 0;
     uint32_t s;
     do {
-        s = src[ip];
+        s = in_byte<STAGE>(L, ip);
         ++ip;
         len += s;
         if (ip > ilimit) return false;
@@ -387,7 +423,7 @@ __device__ __noinline__ void dict_match(Lane& L, int64_t op, int64_t off, int64_
 // One sequence of block L.  Deferred copies land in lc / mc.
 template <bool DICT, bool STAGE>
 __device__ __forceinline__ void decode_step(Lane& L, Copy& lc, Copy& mc) {
-    const u32x4 w = ld16_guarded(L.src + L.ip, L.iend - L.ip);
+    const u32x4 w = in16<STAGE>(L, L.ip);
     const uint32_t tok = w.x & 0xFFu;
     int64_t ip = L.ip + 1;
     int64_t op = L.op;
@@ -400,7 +436,7 @@ __device__ __forceinline__ void decode_step(Lane& L, Copy& lc, Copy& mc) {
 
     if (L.fast) {   // lz4.c:1996-2109
         if (lit == 15) {
-            if (!read_len(L.src, ip, iend - 15, true, add)) goto fail;
+            if (!read_len<STAGE>(L, ip, iend - 15, true, add)) goto fail;
             lit += add;
             if (op + lit > oend - 32 || ip + lit > iend - 32) {
                 L.fast = false;
@@ -410,7 +446,7 @@ __device__ __forceinline__ void decode_step(Lane& L, Copy& lc, Copy& mc) {
             deferred = lc.kind != kNone;
             ip += lit;
             op += lit;
-            off = ld16le(L.src + ip);
+            off = in_le16<STAGE>(L, ip);
         } else {
             if (ip > iend - 17) {
                 L.fast = false;
@@ -418,14 +454,14 @@ __device__ __forceinline__ void decode_step(Lane& L, Copy& lc, Copy& mc) {
             }
             // literals are bytes 1..lit of the token window
             window_literal<STAGE>(L, op, w, lit);
-            off = lit <= 13 ? (window_dword(w, (uint32_t)(1 + lit)) & 0xFFFFu) : ld16le(L.src + ip + lit);
+            off = lit <= 13 ? (window_dword(w, (uint32_t)(1 + lit)) & 0xFFFFu) : in_le16<STAGE>(L, ip + lit);
             ip += lit;
             op += lit;
         }
         ip += 2;
         ml = tok & 15;
         if (ml == 15) {
-            if (!read_len(L.src, ip, iend - 4, false, add)) goto fail;
+            if (!read_len<STAGE>(L, ip, iend - 4, false, add)) goto fail;
             ml += add + 4;
             if (OOW(off)) goto fail;
             if (op + ml >= oend - 64) {
@@ -460,7 +496,7 @@ __device__ __forceinline__ void decode_step(Lane& L, Copy& lc, Copy& mc) {
     // safe phase, lz4.c:2114-2329
     if (lit != 15 && ip < iend - 16 && op <= oend - 32) {   // shortcut, lz4.c:2128-2158
         window_literal<STAGE>(L, op, w, lit);
-        off = lit <= 13 ? (window_dword(w, (uint32_t)(1 + lit)) & 0xFFFFu) : ld16le(L.src + ip + lit);
+        off = lit <= 13 ? (window_dword(w, (uint32_t)(1 + lit)) & 0xFFFFu) : in_le16<STAGE>(L, ip + lit);
         op += lit;
         ip += lit + 2;
         ml = tok & 15;
@@ -476,7 +512,7 @@ __device__ __forceinline__ void decode_step(Lane& L, Copy& lc, Copy& mc) {
         goto match_length;
     }
     if (lit == 15) {
-        if (!read_len(L.src, ip, iend - 15, true, add)) goto fail;
+        if (!read_len<STAGE>(L, ip, iend - 15, true, add)) goto fail;
         lit += add;
     }
 literal_tail:   // lz4.c:2172-2229
@@ -493,12 +529,12 @@ literal_tail:   // lz4.c:2172-2229
     deferred = lc.kind != kNone;
     ip += lit;
     op += lit;
-    off = ld16le(L.src + ip);
+    off = in_le16<STAGE>(L, ip);
     ip += 2;
     ml = tok & 15;
 match_length:   // lz4.c:2238-2245
     if (ml == 15) {
-        if (!read_len(L.src, ip, iend - 4, false, add)) goto fail;
+        if (!read_len<STAGE>(L, ip, iend - 4, false, add)) goto fail;
         ml += add;
     }
     ml += 4;
@@ -700,7 +736,8 @@ __device__ __forceinline__ void fast_exec(Lane& L, u32x4 w, const FastSeq& f) {
 // `slow_batch` lanes wait (or none can go fast) -- one general decode_step
 // for the waiting lanes.  Batching keeps the rarely needed general state
 // machine (and its divergence) off most iterations.
-__global__ __launch_bounds__(256) void stage_decompress_kernel(const uint8_t* __restrict__ src,
+// 4 waves per SIMD (<= 128 VGPRs): the LDS allows 16 waves per CU
+__global__ __launch_bounds__(256, 4) void stage_decompress_kernel(const uint8_t* __restrict__ src,
                                                                const int64_t* __restrict__ src_off,
                                                                const int32_t* __restrict__ src_len, uint8_t* dst,
                                                                const int64_t* __restrict__ dst_off,

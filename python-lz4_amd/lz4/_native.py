@@ -17,6 +17,8 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "_lz4m.so")
+if os.environ.get("LZ4M_LIB"):   # dev hook: an alternative build of the same library (A/B runs)
+    LIB_PATH = os.environ["LZ4M_LIB"]
 
 TABLE_U16_HASH4 = 0
 TABLE_U32_HASH5 = 1

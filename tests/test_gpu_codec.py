@@ -271,3 +271,20 @@ def test_parallel_parse_decoded_by_gpu(gpu, corpus):
     res = gpu_decompress(got, [len(b) for b in src], gpu)
     for i, (s, out) in enumerate(res):
         assert s == len(src[i]) and out == src[i], i
+
+
+@pytest.mark.parametrize("kind", ["text", "source", "markup", "records", "runs", "random"])
+@pytest.mark.parametrize("block", [65536, 4 << 20, 300_001])
+def test_decompress_kinds_and_sizes(gpu, oracle, kind, block):
+    """The hot decoder on every corpus kind at 64 KiB, 4 MiB and an odd
+    block size: long matches (markup: ml > 16 on 70 % of sequences), offsets
+    around the LDS ring's reach, runs and incompressible blocks, positions
+    beyond 64 KiB.  Blocks come from the oracle (LZ4_compress_default);
+    output and status must equal the original bytes and size."""
+    n = 48 if block == 65536 else 3
+    raw = _synth.blocks(n * block // 65536 + 1, kind, seed=31).tobytes()
+    blocks = [raw[i * block:(i + 1) * block] for i in range(n)]
+    comp = [oracle.compress(b) for b in blocks]
+    got = gpu_decompress(comp, [block] * n, gpu)
+    for (st, out), b in zip(got, blocks):
+        assert st == len(b) and out == b

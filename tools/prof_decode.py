@@ -24,13 +24,26 @@ for kind in kinds:
     st = torch.empty(n, dtype=torch.int32, device=dev)
     N.launch_decompress(slots, soff, olen, dst, doff, dcap, st, n)
     torch.cuda.synchronize()
-    assert torch.equal(dst, src)
+    if not os.environ.get("PROF_NOCHECK"):
+        assert torch.equal(dst, src)
     ts = []
     for _ in range(reps):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(); N.launch_decompress(slots, soff, olen, dst, doff, dcap, st, n); b.record()
         torch.cuda.synchronize(); ts.append(a.elapsed_time(b))
     ms = min(ts)
+    if os.environ.get("LZ4M_STATS"):
+        w = list(N._WORK.values())[0].view(torch.int64).cpu().tolist()
+        it, live, fast, slow, slanes, coop, refill = w[1:8]
+        if os.environ.get("LZ4M_STATS") == "2":
+            tot = sum(w[8:13])
+            print(kind, "cycle shares: exec %.2f room+window %.2f parse %.2f slow %.2f refill %.2f; cycles/round %.0f" %
+                  tuple([x / tot for x in w[8:13]] + [tot / max(1, it)]), flush=True)
+            print(kind, "slow-step split: decode_step %.2f final-wait %.2f (of all cycles); cycles per slow step %.0f" %
+                  (w[13] / tot, w[14] / tot, w[11] / max(1, slow)), flush=True)
+        print(kind, f"waves-iter {it} live/iter {live/it:.1f} fast/iter {fast/it:.1f} slow-steps {slow} "
+              f"({slow/it:.3f}/iter, {slanes/max(1,slow):.1f} lanes) coop {coop} refills {refill} "
+              f"fast-lane-seqs/block {fast/n:.0f} iters/block-lane {it*64/n:.0f}", flush=True)
     out[kind] = {"ms": round(ms, 3), "ratio": round(n * 65536 / cbytes, 3), "GiB_s": round(n * 65536 / ms / 1e-3 / 2**30, 1),
                  "algo_GB_s": round((cbytes + n * 65536) / ms / 1e6, 1)}
     print(kind, out[kind], flush=True)
