@@ -7,7 +7,7 @@ OUT=$(realpath -m "$1")
 REPO=$(cd "$(dirname "$0")/.." && pwd)
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-ARGS="--steps 1 --warmup 0 --no-cpu --no-compress --e2e-blocks 0 --random-blocks 131072"
+ARGS="--steps 1 --warmup 0 --no-cpu --no-compress --e2e-blocks 0 --frame-gib 0 --random-blocks 131072"
 i=0
 while read -r grp; do
   [ -z "$grp" ] && continue
