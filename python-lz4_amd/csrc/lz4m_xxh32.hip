@@ -33,8 +33,10 @@ __global__ __launch_bounds__(256) void xxh32_batch_kernel(const uint8_t* __restr
 // step t the accumulator sits in lane t, which holds stripe t's word, and a
 // DPP wave rotate (wave_ror:1, folded into the add) moves it one lane up per
 // step.  Each step is three dependent VALU instructions (add, alignbit,
-// mul) with no v_readlane.  Measured 1.7 GB/s (MI355X); the serial chain is
-// the bound (a scalar-unit version ran at 0.47 GB/s).
+// mul) with no v_readlane.  16 KiB of loads stay in flight.  Measured
+// 1.70 GB/s on 4 GiB (MI355X); the serial chain is the bound (a scalar-unit
+// version ran at 0.47 GB/s; rotating the words to lane 0 instead of the
+// accumulator, 1.44 GB/s).
 __global__ __launch_bounds__(256) void xxh32_long_kernel(const uint8_t* __restrict__ src, int64_t len, uint32_t seed,
                                                          uint32_t* __restrict__ out) {
     __shared__ uint32_t accs[4];
@@ -43,7 +45,7 @@ __global__ __launch_bounds__(256) void xxh32_long_kernel(const uint8_t* __restri
     const uint32_t init[4] = {seed + kP1 + kP2, seed + kP2, seed, seed - kP1};
     uint32_t acc = wave == 0 ? init[0] : wave == 1 ? init[1] : wave == 2 ? init[2] : init[3];
     constexpr int64_t kChunk = 16 * kWave;
-    constexpr int kD = 4;
+    constexpr int kD = 16;   // 16 KiB in flight: HBM latency hides behind 1024 chain steps
     const int64_t nk = len / kChunk;
     u32x4 buf[kD];
 #pragma unroll

@@ -5,7 +5,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "python-lz4_amd"))
 from lz4 import _native as N
 dev = torch.device("cuda", 0)
-L = 1 << 30
+L = 4 << 30
 buf = torch.randint(0, 255, (L + 4,), dtype=torch.uint8, device=dev)
 out = torch.empty(1, dtype=torch.int32, device=dev)
 for sh in (0, 1):
