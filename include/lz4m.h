@@ -174,6 +174,21 @@ int lz4m_frame_emit(const uint8_t* d_raw, const int64_t* d_raw_off, const int32_
                     uint8_t* d_frame, const int64_t* d_frame_off, int block_checksum,
                     int64_t n, lz4m_stream_t stream);
 
+/*
+ * Block-record walk of an LZ4 frame already in device memory
+ * (LZ4F_decompress, lz4frame.c:1643-1701 and 1926-1965): starting at the
+ * first record (`pos` = header size), records k = 0.. get d_rec_pos[k] (the
+ * payload position), d_rec_len[k] (stored size) and d_rec_raw[k] (bit 31 of
+ * the record header: stored uncompressed).  d_result[4] = {records, state,
+ * end position, content-checksum position or -1}; state 0 = complete frame,
+ * 1 = incomplete, 2 = block size above max_block, 3 = content checksum
+ * missing, 4 = more than max_rec records.  Serial over records (one lane).
+ * Serves lz4.frame.decompress_device (device-resident frames).
+ */
+int lz4m_frame_scan(const uint8_t* d_frame, int64_t frame_len, int64_t pos, int block_checksum,
+                    int content_checksum, int32_t max_block, int64_t max_rec, int64_t* d_rec_pos,
+                    int32_t* d_rec_len, uint8_t* d_rec_raw, int64_t* d_result, lz4m_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

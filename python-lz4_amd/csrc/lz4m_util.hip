@@ -169,6 +169,66 @@ __global__ __launch_bounds__(256) void frame_block_crc_kernel(uint8_t* __restric
     d[L + 3] = (uint8_t)(c >> 24);
 }
 
+
+// LZ4F_decompress's walk over the block records of a frame already in HBM
+// (lz4frame.c:1643-1701 block headers, 1926-1965 endmark and content
+// checksum).  Serial by construction -- each record's position depends on
+// the previous one's size -- so one lane walks it: one dependent HBM read per
+// record (~1-2 us; 2 048 records of an 8 GiB, 4 MiB-block frame take a few
+// ms).  result = {records, state, end, content-checksum position}; state 0 =
+// complete frame, 1 = incomplete, 2 = block size above the maximum, 3 =
+// content checksum missing, 4 = more than max_rec records.
+__global__ void frame_scan_kernel(const uint8_t* __restrict__ frame, int64_t n, int64_t pos, int crc,
+                                  int content_checksum, int32_t max_block, int64_t max_rec,
+                                  int64_t* __restrict__ rec_pos, int32_t* __restrict__ rec_len,
+                                  uint8_t* __restrict__ rec_raw, int64_t* __restrict__ result) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    int64_t k = 0, state = 0, end = 0, cpos = -1;
+    while (true) {
+        if (n - pos < 4) {
+            state = 1;
+            break;
+        }
+        const uint32_t hdr = ld32(frame + pos);
+        pos += 4;
+        if (hdr == 0) {   // endmark
+            if (content_checksum) {
+                if (n - pos < 4) {
+                    state = 3;
+                    break;
+                }
+                cpos = pos;
+                end = pos + 4;
+            } else {
+                end = pos;
+            }
+            break;
+        }
+        const int64_t size = hdr & 0x7FFFFFFFu;
+        if (size > max_block) {
+            state = 2;
+            break;
+        }
+        if (n - pos < size + crc) {
+            state = 1;
+            break;
+        }
+        if (k == max_rec) {
+            state = 4;
+            break;
+        }
+        rec_pos[k] = pos;
+        rec_len[k] = (int32_t)size;
+        rec_raw[k] = (uint8_t)(hdr >> 31);
+        ++k;
+        pos += size + crc;
+    }
+    result[0] = k;
+    result[1] = state;
+    result[2] = end;
+    result[3] = cpos;
+}
+
 }  // namespace lz4m
 
 using namespace lz4m;
@@ -220,6 +280,16 @@ extern "C" int lz4m_frame_emit(const uint8_t* d_raw, const int64_t* d_raw_off, c
     if (block_checksum)
         hipLaunchKernelGGL(frame_block_crc_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, d_frame,
                            d_frame_off, d_raw_len, d_cmp_len, n);
+    return (int)hipGetLastError();
+}
+
+extern "C" int lz4m_frame_scan(const uint8_t* d_frame, int64_t frame_len, int64_t pos, int block_checksum,
+                               int content_checksum, int32_t max_block, int64_t max_rec, int64_t* d_rec_pos,
+                               int32_t* d_rec_len, uint8_t* d_rec_raw, int64_t* d_result, lz4m_stream_t stream) {
+    if (frame_len < 0 || pos < 0 || max_block < 0 || max_rec < 0 || !d_result) return LZ4M_EINVAL;
+    hipLaunchKernelGGL(frame_scan_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, d_frame, frame_len, pos,
+                       block_checksum ? 4 : 0, content_checksum, max_block, max_rec, d_rec_pos, d_rec_len, d_rec_raw,
+                       d_result);
     return (int)hipGetLastError();
 }
 

@@ -50,6 +50,7 @@ def _declare(lib) -> None:
         "lz4m_gather": ([vp, vp, vp, vp, vp, i64, vp], i32),
         "lz4m_frame_block_sizes": ([vp, vp, i32, vp, i64, vp], i32),
         "lz4m_frame_emit": ([vp, vp, vp, vp, vp, vp, vp, vp, i32, i64, vp], i32),
+        "lz4m_frame_scan": ([vp, i64, i64, i32, i32, i32, i64, vp, vp, vp, vp, vp], i32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)
@@ -177,6 +178,14 @@ def frame_emit(raw, raw_off, raw_len, cmp, cmp_off, cmp_len, frame, frame_off, b
     rc = lib().lz4m_frame_emit(ptr(raw), ptr(raw_off), ptr(raw_len), ptr(cmp), ptr(cmp_off), ptr(cmp_len),
                                ptr(frame), ptr(frame_off), int(bool(block_checksum)), n, stream_ptr(stream))
     check(rc, "lz4m_frame_emit")
+
+
+def frame_scan(frame, frame_len, pos, block_checksum, content_checksum, max_block, max_rec, rec_pos, rec_len,
+               rec_raw, result, stream=None) -> None:
+    rc = lib().lz4m_frame_scan(ptr(frame), frame_len, pos, int(bool(block_checksum)), int(bool(content_checksum)),
+                               max_block, max_rec, ptr(rec_pos), ptr(rec_len), ptr(rec_raw), ptr(result),
+                               stream_ptr(stream))
+    check(rc, "lz4m_frame_scan")
 
 
 # ------------------------------------------------------------ host <-> device

@@ -7,6 +7,7 @@ LZ4FrameFile, ...) is outside this codec's scope.
 from ._frame import (  # noqa: F401
     compress,
     compress_device,
+    decompress_device,
     decompress,
     get_frame_info,
     BLOCKSIZE_DEFAULT,

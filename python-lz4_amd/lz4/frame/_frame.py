@@ -301,74 +301,93 @@ def decompress(data, return_bytearray=False, return_bytes_read=False):
         out = bytearray() if return_bytearray else b""
         return (out, end) if return_bytes_read else out
     recs, state = _scan_blocks(mv, hsize, info)
-    dec = "LZ4F_decompress"
     dev = N.device()
     nb = len(recs)
-    maxb = info["block_size"]
-    out_t = None
-    total = 0
-    first_err = None          # (block index, code)
+    out_t, total, first_err = None, 0, None
     if nb:
         d_frame = N.to_device(mv, dev, pad=16)
-        cpos = [r[1] for r in recs]
-        clen = [r[2] for r in recs]
-        is_raw = [r[0] for r in recs]
-        # block checksums (of the stored payload), verified first per block
-        crc_bad = [False] * nb
-        if info["block_checksum"]:
-            sums = torch.empty(nb, dtype=torch.int32, device=dev)
-            N.launch_xxh32_batch(d_frame, torch.tensor(cpos, dtype=torch.int64, device=dev),
-                                 torch.tensor(clen, dtype=torch.int64, device=dev), 0, sums, nb)
-            got = [v & 0xFFFFFFFF for v in sums.cpu().tolist()]
-            for i, r in enumerate(recs):
-                if got[i] != struct.unpack_from("<I", mv, r[3])[0]:
-                    crc_bad[i] = True
-        slots = torch.empty(nb * maxb + 16, dtype=torch.uint8, device=dev)
-        slot_off = torch.arange(nb, dtype=torch.int64, device=dev) * maxb
-        c_off = torch.tensor(cpos, dtype=torch.int64, device=dev)
-        c_len = torch.tensor(clen, dtype=torch.int32, device=dev)
-        raw_mask = torch.tensor(is_raw, dtype=torch.bool, device=dev)
-        status = torch.empty(nb, dtype=torch.int32, device=dev)
-        caps = torch.full((nb,), maxb, dtype=torch.int32, device=dev)
-        if info["block_linked"] and nb > 1 and not all(is_raw):
-            _decode_linked(d_frame, c_off, c_len, raw_mask, slots, status, maxb)
-            sizes = status.cpu().tolist()
-            dst_off_list = None
-        else:
-            # raw blocks are handed to the decoder with length 0 (immediate
-            # reject, no work); they are gathered from the frame below
-            dec_len = torch.where(raw_mask, torch.zeros_like(c_len), c_len)
-            N.launch_decompress(d_frame, c_off, dec_len, slots, slot_off, caps, status, nb)
-            sizes = status.cpu().tolist()
-            for i in range(nb):
-                if is_raw[i]:
-                    sizes[i] = clen[i]
-            dst_off_list = None
-        for i in range(nb):
-            if crc_bad[i]:
-                first_err = (i, "blockChecksum_invalid")
-                break
-            if not is_raw[i] and sizes[i] < 0:
-                first_err = (i, "decompressionFailed")
-                break
-        if first_err is None:
-            if info["block_linked"] and nb > 1 and not all(is_raw):
-                total = sum(sizes)
-                out_t = slots                                  # already contiguous
-            else:
-                lens = torch.tensor(sizes, dtype=torch.int32, device=dev)
-                src_off = torch.where(raw_mask, c_off, slot_off)
-                src_buf_is_frame = raw_mask
-                offs = N.exclusive_scan(lens)
-                total = int(offs[-1].item())
-                out_t = torch.empty(total + 16, dtype=torch.uint8, device=dev)
-                # compressed blocks from the slots, raw blocks from the frame
-                sel_c = torch.nonzero(~src_buf_is_frame).flatten()
-                sel_r = torch.nonzero(src_buf_is_frame).flatten()
-                if sel_c.numel():
-                    N.gather(slots, slot_off[sel_c], lens[sel_c], out_t, offs[sel_c], sel_c.numel())
-                if sel_r.numel():
-                    N.gather(d_frame, c_off[sel_r], lens[sel_r], out_t, offs[sel_r], sel_r.numel())
+        t = lambda v, dt: torch.tensor(v, dtype=dt, device=dev)   # noqa: E731
+        out_t, total, first_err = _decode_records(
+            d_frame, info, nb, t([r[1] for r in recs], torch.int64), t([r[2] for r in recs], torch.int32),
+            t([r[0] for r in recs], torch.bool), t([r[3] for r in recs], torch.int64))
+    _frame_errors(first_err, state, info, total)
+    bytes_read = state[1]
+    if info["content_checksum"]:
+        want = struct.unpack_from("<I", mv, state[2])[0]
+        got = _xxh32_dev(out_t, total) if total else _xxh32_dev(b"")
+        if got != want:
+            raise _err("LZ4F_decompress", "contentChecksum_invalid")
+    out = N.to_host_bytes(out_t, total, bool(return_bytearray)) if total else (bytearray() if return_bytearray else b"")
+    if return_bytes_read:
+        return out, bytes_read
+    return out
+
+
+def decompress_device(d_frame: torch.Tensor, n: int | None = None, stream=None) -> torch.Tensor:
+    """Device-resident LZ4F_decompress: decode the frame in d_frame[:n] (a
+    uint8 device tensor) into a new uint8 device tensor, with no host copy of
+    the data (BASELINE config 4).  The header is parsed on
+    the host from its first bytes; the block records are walked on the device
+    (lz4m_frame_scan); independent blocks decode in one batched launch, linked
+    ones on the chain kernel; block and content checksums are verified on the
+    device.  A malformed or truncated frame raises exactly what
+    ``decompress`` raises for the same bytes."""
+    n = d_frame.numel() if n is None else int(n)
+    dev = d_frame.device
+    head = bytes(d_frame[: min(n, 19)].cpu().numpy().tobytes())
+    try:
+        info, hsize = _parse_header(memoryview(head))
+    except RuntimeError:
+        if n <= 19:
+            raise
+        info, hsize = None, 0
+    if info is None or info["skippable"] or n <= hsize:
+        # errors and skippable frames: the host path's exact semantics
+        out = decompress(d_frame[:n].cpu().numpy().tobytes())
+        return torch.frombuffer(bytearray(out), dtype=torch.uint8).to(dev) if out else \
+            torch.empty(0, dtype=torch.uint8, device=dev)
+    crc = 4 if info["block_checksum"] else 0
+    max_rec = n // 64 + 1024
+    rec_pos = torch.empty(max_rec, dtype=torch.int64, device=dev)
+    rec_len = torch.empty(max_rec, dtype=torch.int32, device=dev)
+    rec_raw = torch.empty(max_rec, dtype=torch.uint8, device=dev)
+    res = torch.zeros(4, dtype=torch.int64, device=dev)
+    N.frame_scan(d_frame, n, hsize, info["block_checksum"], info["content_checksum"], info["block_size"], max_rec,
+                 rec_pos, rec_len, rec_raw, res, stream)
+    nb, st, _end, cpos = (int(v) for v in res.cpu().tolist())
+    if st != 0:   # malformed / truncated (or > max_rec records): the host path's exact result or error
+        out = decompress(d_frame[:n].cpu().numpy().tobytes())
+        return torch.frombuffer(bytearray(out), dtype=torch.uint8).to(dev) if out else \
+            torch.empty(0, dtype=torch.uint8, device=dev)
+    out_t, total, first_err = None, 0, None
+    if nb:
+        crc_pos = rec_pos[:nb] + rec_len[:nb].to(torch.int64) if crc else torch.full((nb,), -1, dtype=torch.int64,
+                                                                                      device=dev)
+        out_t, total, first_err = _decode_records(d_frame, info, nb, rec_pos[:nb], rec_len[:nb],
+                                                  rec_raw[:nb].to(torch.bool), crc_pos)
+    _frame_errors(first_err, ("end", _end, cpos if cpos >= 0 else None), info, total)
+    if info["content_checksum"]:
+        want = int(_le32_at(d_frame, torch.tensor([cpos], dtype=torch.int64, device=dev)).item()) & 0xFFFFFFFF
+        got = _xxh32_dev(out_t, total) if total else _xxh32_dev(b"")
+        if got != want:
+            raise _err("LZ4F_decompress", "contentChecksum_invalid")
+    if not total:
+        return torch.empty(0, dtype=torch.uint8, device=dev)
+    return out_t[:total]
+
+
+def _le32_at(d_buf, pos):
+    """LE32 values at device positions `pos` of d_buf (int64 tensor)."""
+    idx = pos[:, None] + torch.arange(4, dtype=torch.int64, device=pos.device)
+    b = d_buf[idx].to(torch.int64)
+    return b[:, 0] | (b[:, 1] << 8) | (b[:, 2] << 16) | (b[:, 3] << 24)
+
+
+def _frame_errors(first_err, state, info, total):
+    """The error order of __decompress / LZ4F_decompress (lz4frame.c:1819,
+    1844-1847, 1927): first failing block, then a structural error, then
+    truncation, then the content size."""
+    dec = "LZ4F_decompress"
     if first_err is not None:
         raise _err(dec, first_err[1])
     if state[0] == "error":
@@ -379,16 +398,52 @@ def decompress(data, return_bytearray=False, return_bytes_read=False):
         raise _err(dec, "frameSize_wrong")                     # lz4frame.c:1927
     if state[0] == "incomplete_suffix":
         raise RuntimeError(f"Frame incomplete. LZ4F_decompress returned: {state[1]}")
-    bytes_read = state[1]
-    if info["content_checksum"]:
-        want = struct.unpack_from("<I", mv, state[2])[0]
-        got = _xxh32_dev(out_t, total) if total else _xxh32_dev(b"")
-        if got != want:
-            raise _err(dec, "contentChecksum_invalid")
-    out = N.to_host_bytes(out_t, total, bool(return_bytearray)) if total else (bytearray() if return_bytearray else b"")
-    if return_bytes_read:
-        return out, bytes_read
-    return out
+
+
+def _decode_records(d_frame, info, nb, c_off, c_len, raw_mask, crc_pos):
+    """Decode nb block records of a frame in device memory: payload at
+    c_off[i] (int64), stored size c_len[i] (int32), raw_mask[i] = stored
+    uncompressed, crc_pos[i] = position of its LE32 block checksum or -1.
+    Returns (out tensor, total decoded bytes, first error or None)."""
+    dev = d_frame.device
+    maxb = info["block_size"]
+    status = torch.empty(nb, dtype=torch.int32, device=dev)
+    crc_bad = None
+    if info["block_checksum"]:                                 # lz4frame.c:1819: verified first per block
+        sums = torch.empty(nb, dtype=torch.int32, device=dev)
+        N.launch_xxh32_batch(d_frame, c_off, c_len.to(torch.int64), 0, sums, nb)
+        crc_bad = (sums.to(torch.int64) & 0xFFFFFFFF) != _le32_at(d_frame, crc_pos)
+    slots = torch.empty(nb * maxb + 16, dtype=torch.uint8, device=dev)
+    slot_off = torch.arange(nb, dtype=torch.int64, device=dev) * maxb
+    linked = info["block_linked"] and nb > 1 and not bool(raw_mask.all())
+    if linked:
+        _decode_linked(d_frame, c_off, c_len, raw_mask, slots, status, maxb)
+    else:
+        # raw blocks are handed to the decoder with length 0 (immediate
+        # reject, no work); they are gathered from the frame below
+        caps = torch.full((nb,), maxb, dtype=torch.int32, device=dev)
+        dec_len = torch.where(raw_mask, torch.zeros_like(c_len), c_len)
+        N.launch_decompress(d_frame, c_off, dec_len, slots, slot_off, caps, status, nb)
+    sizes = torch.where(raw_mask, c_len, status) if not linked else status
+    bad_dec = (~raw_mask) & (status < 0)
+    bad = bad_dec if crc_bad is None else (bad_dec | crc_bad)
+    if bool(bad.any()):
+        i = int(torch.nonzero(bad).flatten()[0])
+        code = "blockChecksum_invalid" if crc_bad is not None and bool(crc_bad[i]) else "decompressionFailed"
+        return None, 0, (i, code)
+    if linked:
+        return slots, int(sizes.to(torch.int64).sum()), None
+    lens = sizes.to(torch.int32)
+    offs = N.exclusive_scan(lens)
+    total = int(offs[-1].item())
+    out_t = torch.empty(total + 16, dtype=torch.uint8, device=dev)
+    sel_c = torch.nonzero(~raw_mask).flatten()
+    sel_r = torch.nonzero(raw_mask).flatten()
+    if sel_c.numel():                                          # compressed blocks from the slots
+        N.gather(slots, slot_off[sel_c], lens[sel_c], out_t, offs[sel_c], sel_c.numel())
+    if sel_r.numel():                                          # raw blocks straight from the frame
+        N.gather(d_frame, c_off[sel_r], lens[sel_r], out_t, offs[sel_r], sel_r.numel())
+    return out_t, total, None
 
 
 def _decode_linked(d_frame, c_off, c_len, raw_mask, out, status, maxb):

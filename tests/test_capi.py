@@ -20,7 +20,8 @@ def test_header_declares_entry_points():
     syms = declared_symbols()
     for s in ["lz4m_decompress_batch", "lz4m_decompress_batch_dict", "lz4m_decompress_chain",
               "lz4m_compress_batch", "lz4m_xxh32_batch", "lz4m_xxh32_long", "lz4m_compress_bound",
-              "lz4m_exclusive_scan", "lz4m_gather", "lz4m_frame_emit", "lz4m_frame_block_sizes"]:
+              "lz4m_exclusive_scan", "lz4m_gather", "lz4m_frame_emit", "lz4m_frame_block_sizes",
+              "lz4m_frame_scan"]:
         assert s in syms, s
 
 
@@ -51,6 +52,8 @@ def test_argument_validation_without_gpu():
     assert lib.lz4m_compress_batch(None, None, None, None, None, None, None, -5, 0, 1, None) == N.EINVAL
     assert lib.lz4m_xxh32_batch(None, None, None, 0, None, -1, None) == N.EINVAL
     assert lib.lz4m_xxh32_long(None, -1, 0, None, None) == N.EINVAL
+    assert lib.lz4m_frame_scan(None, -1, 0, 0, 0, 65536, 1, None, None, None, None, None) == N.EINVAL
+    assert lib.lz4m_frame_scan(None, 16, 0, 0, 0, 65536, 1, None, None, None, None, None) == N.EINVAL
 
 
 def test_no_cpu_fallback():

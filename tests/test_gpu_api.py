@@ -295,3 +295,71 @@ def test_frame_trailing_data_and_multiframe(gpu):
     d, n = lz4.frame.decompress(ca + cb, return_bytes_read=True)
     assert d == a and n == len(ca)
     assert lz4.frame.decompress((ca + cb)[n:]) == b
+
+
+# -------------------------------------------------- device-resident frames
+def _dev(b, gpu):
+    import torch
+    return torch.frombuffer(bytearray(b), dtype=torch.uint8).to(gpu) if len(b) else \
+        torch.empty(0, dtype=torch.uint8, device=gpu)
+
+
+@pytest.mark.parametrize("data", FRAME_DATA[:5], ids=[f"f{i}" for i in range(5)])
+@pytest.mark.parametrize("block_size", [4, 7])
+@pytest.mark.parametrize("block_linked", [True, False])
+@pytest.mark.parametrize("checksums", [(False, False), (True, True)])
+def test_frame_decompress_device_roundtrip(gpu, data, block_size, block_linked, checksums):
+    """lz4.frame.decompress_device (device record walk, batched decode,
+    device checksum checks) returns what lz4.frame.decompress returns."""
+    cc, bc = checksums
+    c = lz4.frame.compress(data, block_size=block_size, block_linked=block_linked, content_checksum=cc,
+                           block_checksum=bc)
+    out = lz4.frame.decompress_device(_dev(c, gpu))
+    assert out.is_cuda and out.cpu().numpy().tobytes() == bytes(data)
+
+
+def test_frame_decompress_device_reference_frames(gpu, golden):
+    """Frames made by the reference LZ4F_compressFrame (golden vectors)."""
+    man, arr = golden
+    inputs = {e["name"]: _b(arr, e["key"]) for e in man["inputs"]}
+    for e in man["frames"]:
+        out = lz4.frame.decompress_device(_dev(_b(arr, e["key"]), gpu))
+        assert out.cpu().numpy().tobytes() == inputs[e["input"]], e["opts"]
+
+
+def test_frame_decompress_device_errors(gpu):
+    """Malformed device frames raise exactly what the host path raises."""
+    data = os.urandom(256 * 1024)
+    c = lz4.frame.compress(data, content_checksum=True, block_checksum=True, return_bytearray=True)
+    bad_crc = bytearray(c)
+    bad_crc[22] ^= 0x42
+    with pytest.raises(RuntimeError, match=r"^LZ4F_decompress failed with code: ERROR_blockChecksum_invalid$"):
+        lz4.frame.decompress_device(_dev(bad_crc, gpu))
+    bad_content = bytearray(c)
+    bad_content[-1] ^= 0x42
+    with pytest.raises(RuntimeError, match=r"^LZ4F_decompress failed with code: ERROR_contentChecksum_invalid$"):
+        lz4.frame.decompress_device(_dev(bad_content, gpu))
+    for i in (6, 16, 5000, len(c) - 3):
+        with pytest.raises(RuntimeError) as e:
+            lz4.frame.decompress_device(_dev(c[:i], gpu))
+        with pytest.raises(RuntimeError) as h:
+            lz4.frame.decompress(bytes(c[:i]))
+        assert str(e.value) == str(h.value)
+    bad = bytearray(c)
+    bad[0] ^= 1
+    with pytest.raises(RuntimeError, match="ERROR_frameType_unknown"):
+        lz4.frame.decompress_device(_dev(bad, gpu))
+
+
+def test_frame_device_roundtrip_large_blocks(gpu):
+    """compress_device -> decompress_device without leaving the GPU
+    (config 4 shape: 4 MiB independent blocks, content checksum)."""
+    import torch
+    from lz4 import _synth
+    data = _synth.blocks(160, "silesia", seed=12).tobytes()
+    d = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(gpu)
+    for parse in ("exact", "parallel"):
+        f = lz4.frame.compress_device(d, block_size=lz4.frame.BLOCKSIZE_MAX4MB, block_linked=False,
+                                      content_checksum=True, parse=parse)
+        out = lz4.frame.decompress_device(f)
+        assert torch.equal(out, d)
