@@ -189,7 +189,14 @@ def main():
         c3 = {"compress_gib_s": round(world * n * BLOCK / (c_wall / max(1, args.steps // 2)) / GIB, 2),
               "compress_kernel_ms": round(c_ev * 1e3, 3),
               "compress_ratio": round(n * BLOCK / par_total, 4),
-              "compress_algo_gbs": round((n * BLOCK + par_total) / c_ev / 1e9, 1)}
+              "compress_algo_gbs": round((n * BLOCK + par_total) / c_ev / 1e9, 1),
+              "compress_parse": "parallel, 12-bit hash table (LZ4M_PARSE_PARALLEL)"}
+        # the same parse with the reference's 13-bit table (LZ4M_PARSE_PARALLEL_HQ)
+        h_wall, h_ev = time_kernel(lambda: N.launch_compress(src, src_off, src_len, slots, slot_off, slot_cap,
+                                                             out_len, n, N.PARSE_PARALLEL_HQ, 1), 1, 0, world)
+        assert int((out_len <= 0).sum()) == 0, "parallel (HQ) compress failed on some block"
+        c3["compress_hq_gib_s"] = round(world * n * BLOCK / h_wall / GIB, 2)
+        c3["compress_hq_ratio"] = round(n * BLOCK / int(out_len.to(torch.int64).sum()), 4)
 
     log("[bench] parallel compress done")
     # ---- decode input: the exact LZ4_compress_default parse (byU16/hash4) ----
@@ -202,6 +209,7 @@ def main():
     ratio = n * BLOCK / comp_total
     if c3:
         c3["compress_ratio_vs_default"] = round(c3["compress_ratio"] / ratio, 4)
+        c3["compress_hq_ratio_vs_default"] = round(c3["compress_hq_ratio"] / ratio, 4)
     c3["compress_exact_gib_s"] = round(world * n * BLOCK / x_wall / GIB, 2)
 
     # compact into one contiguous compressed buffer (what a file/socket holds)

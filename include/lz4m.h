@@ -42,11 +42,14 @@ typedef struct ihipStream_t* lz4m_stream_t;   /* == hipStream_t */
 #define LZ4M_TABLE_U32_HASH5 1
 /* pick what LZ4_compress_default would pick for each block's size */
 #define LZ4M_TABLE_AUTO      2
-/* parallel-parse compressor (lz4m_pcompress.hip): a valid block at the ratio
- * of LZ4_compress_default (greedy, full insertion, catch-up), NOT
+/* parallel-parse compressor (lz4m_pcompress.hip): a valid block near the
+ * ratio of LZ4_compress_default (greedy, full insertion, catch-up), NOT
  * byte-identical to it; blocks up to 64 KiB (larger ones get size 0);
- * `acceleration` is ignored.  For bulk compression (BASELINE config 3). */
+ * `acceleration` is ignored.  For bulk compression (BASELINE config 3).
+ * PARALLEL uses a 12-bit hash table (+1.5 % size on the silesia-like mix,
+ * 1.7x the speed), PARALLEL_HQ the reference's 13 bits (-0.02 % size). */
 #define LZ4M_PARSE_PARALLEL  3
+#define LZ4M_PARSE_PARALLEL_HQ 5
 /* the same parse for blocks of any size (32 KiB LDS table of u32 positions,
  * offsets limited to 65535 like LZ4_DISTANCE_MAX); e.g. 4 MiB frame blocks */
 #define LZ4M_PARSE_PARALLEL_LARGE 4

@@ -27,7 +27,7 @@
 namespace lz4m {
 
 int pcompress_launch(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len, uint8_t* d_dst,
-                     const int64_t* d_dst_off, const int32_t* d_dst_cap, int32_t* d_out_len, int64_t n, bool big,
+                     const int64_t* d_dst_off, const int32_t* d_dst_cap, int32_t* d_out_len, int64_t n, int variant,
                      hipStream_t stream);
 
 constexpr int kMinLength = 13;        // lz4.c:247
@@ -381,9 +381,11 @@ extern "C" int lz4m_compress_batch(const uint8_t* d_src, const int64_t* d_src_of
                                d_src_len, d_dst, d_dst_off, d_dst_cap, d_out_len, n, acceleration);
             break;
         case LZ4M_PARSE_PARALLEL:
-            return pcompress_launch(d_src, d_src_off, d_src_len, d_dst, d_dst_off, d_dst_cap, d_out_len, n, false, s);
+            return pcompress_launch(d_src, d_src_off, d_src_len, d_dst, d_dst_off, d_dst_cap, d_out_len, n, 0, s);
+        case LZ4M_PARSE_PARALLEL_HQ:
+            return pcompress_launch(d_src, d_src_off, d_src_len, d_dst, d_dst_off, d_dst_cap, d_out_len, n, 1, s);
         case LZ4M_PARSE_PARALLEL_LARGE:
-            return pcompress_launch(d_src, d_src_off, d_src_len, d_dst, d_dst_off, d_dst_cap, d_out_len, n, true, s);
+            return pcompress_launch(d_src, d_src_off, d_src_len, d_dst, d_dst_off, d_dst_cap, d_out_len, n, 2, s);
         case LZ4M_TABLE_AUTO:
             hipLaunchKernelGGL(compress_kernel_auto, dim3(grid), dim3(64), 0, s, d_src, d_src_off, d_src_len, d_dst,
                                d_dst_off, d_dst_cap, d_out_len, n, acceleration);

@@ -34,7 +34,14 @@ namespace lz4m {
 
 constexpr uint32_t kEmpty = 0xFFFFu;
 
-__device__ __forceinline__ uint32_t phash(uint32_t v) { return (v * 2654435761u) >> 19; }
+// hash of 4 bytes into HB bits (LZ4_hash4, lz4.c:756-762: 13 bits for the
+// byU16 table).  The table is the kernel's whole LDS, and the kernel is
+// latency bound: a 12-bit table (8 KB) fits 20 waves per CU instead of 10
+// and compresses 1.7x faster for +1.5 % size on the silesia-like mix
+// (LZ4M_PARSE_PARALLEL); 13 bits (LZ4M_PARSE_PARALLEL_HQ) keeps the
+// reference's table size and ratio (-0.02 %).
+template <int HB>
+__device__ __forceinline__ uint32_t phash(uint32_t v) { return (v * 2654435761u) >> (32 - HB); }
 
 // equal leading bytes of two 16-byte windows (0..16)
 __device__ __forceinline__ uint32_t eq_prefix16(u32x4 a, u32x4 b) {
@@ -228,12 +235,12 @@ struct Chunk {
     uint32_t bp, bc;  // 4 bytes before p / before cand
 };
 
-template <bool BIG>
+template <bool BIG, int HB>
 __device__ __forceinline__ void chunk_issue(Chunk& C, const uint8_t* s, uint32_t* table32, int32_t p0, uint32_t v,
                                             int32_t N, int32_t mlast, uint32_t lane) {
     const int32_t p = p0 + (int32_t)lane;
     const bool act = p + 4 <= N;
-    const uint32_t h = act ? phash(v) : 8192u;
+    const uint32_t h = act ? phash<HB>(v) : (1u << HB);
     // nearest earlier / later lane with the same hash: bitonic sort of (hash, lane)
     const uint32_t key = wave_sort((h << 6) | lane, lane);
     const uint32_t kprev = (uint32_t)__builtin_amdgcn_update_dpp((int)key, (int)key, 0x138, 0xF, 0xF, false);
@@ -280,7 +287,7 @@ __device__ __forceinline__ uint64_t chunk_finish(const Chunk& C, int32_t p0, int
     return __ballot(ok);
 }
 
-template <bool BIG>
+template <bool BIG, int HB>
 __global__ __launch_bounds__(64) void pcompress_kernel(const uint8_t* __restrict__ src,
                                                        const int64_t* __restrict__ src_off,
                                                        const int32_t* __restrict__ src_len, uint8_t* __restrict__ dst,
@@ -288,7 +295,8 @@ __global__ __launch_bounds__(64) void pcompress_kernel(const uint8_t* __restrict
                                                        const int32_t* __restrict__ dst_cap,
                                                        int32_t* __restrict__ out_len, int64_t n) {
     // 8192 hash4 entries: u16 positions (blocks <= 64 KiB) or u32 (BIG)
-    __shared__ __attribute__((aligned(16))) uint32_t table[BIG ? 8192 : 4096];
+    constexpr int kWords = BIG ? (1 << HB) : (1 << HB) / 2;   // table size in u32 words
+    __shared__ __attribute__((aligned(16))) uint32_t table[kWords];
     const uint32_t lane = threadIdx.x;
     for (int64_t b = blockIdx.x; b < n; b += gridDim.x) {
         const int32_t N = src_len[b];
@@ -299,7 +307,7 @@ __global__ __launch_bounds__(64) void pcompress_kernel(const uint8_t* __restrict
             if (lane == 0) out_len[b] = 0;
             continue;
         }
-        for (int k = (int)lane; k < (BIG ? 8192 : 4096) / 4; k += 64)
+        for (int k = (int)lane; k < kWords / 4; k += 64)
             reinterpret_cast<u32x4*>(table)[k] = u32x4{0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
         int32_t anchor = 0, cur = 0, op = 0;
         bool fail = false;
@@ -310,14 +318,14 @@ __global__ __launch_bounds__(64) void pcompress_kernel(const uint8_t* __restrict
         int32_t L = 0, back = 0;
         uint64_t mask = 0;
         if (N >= 4) {
-            chunk_issue<BIG>(A, s, table, 0, load_word(s, (int32_t)lane, N), N, mlast, lane);
+            chunk_issue<BIG, HB>(A, s, table, 0, load_word(s, (int32_t)lane, N), N, mlast, lane);
             mask = chunk_finish(A, 0, matchlimit, L, back, lane);
         }
         for (int32_t p0 = 0; p0 + 4 <= N; p0 += 64) {
             const bool has_next = p0 + 68 <= N;
             Chunk B;
             if (has_next)
-                chunk_issue<BIG>(B, s, table, p0 + 64, load_word(s, p0 + 64 + (int32_t)lane, N), N, mlast, lane);
+                chunk_issue<BIG, HB>(B, s, table, p0 + 64, load_word(s, p0 + 64 + (int32_t)lane, N), N, mlast, lane);
             // ---- greedy parse of chunk p0
             int ns = 0;
             int32_t q_ls = 0, q_lit = 0, q_off = 0, q_ml = 0, q_ob = 0, q_pb = 0;   // sequence ns in lane ns
@@ -387,16 +395,21 @@ __global__ __launch_bounds__(64) void pcompress_kernel(const uint8_t* __restrict
     }
 }
 
+// variant: 0 = blocks <= 64 KiB, 12-bit u16 table; 1 = the same with 13 bits;
+// 2 = any block size, 13-bit u32 table
 int pcompress_launch(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len, uint8_t* d_dst,
-                     const int64_t* d_dst_off, const int32_t* d_dst_cap, int32_t* d_out_len, int64_t n, bool big,
+                     const int64_t* d_dst_off, const int32_t* d_dst_cap, int32_t* d_out_len, int64_t n, int variant,
                      hipStream_t stream) {
     const uint32_t grid = (uint32_t)(n < (1ll << 30) ? n : (1ll << 30));
-    if (big) {
-        hipLaunchKernelGGL(pcompress_kernel<true>, dim3(grid), dim3(64), 0, stream, d_src, d_src_off, d_src_len,
+    if (variant == 2) {
+        hipLaunchKernelGGL((pcompress_kernel<true, 13>), dim3(grid), dim3(64), 0, stream, d_src, d_src_off, d_src_len,
                            d_dst, d_dst_off, d_dst_cap, d_out_len, n);
+    } else if (variant == 1) {
+        hipLaunchKernelGGL((pcompress_kernel<false, 13>), dim3(grid), dim3(64), 0, stream, d_src, d_src_off,
+                           d_src_len, d_dst, d_dst_off, d_dst_cap, d_out_len, n);
     } else {
-        hipLaunchKernelGGL(pcompress_kernel<false>, dim3(grid), dim3(64), 0, stream, d_src, d_src_off, d_src_len,
-                           d_dst, d_dst_off, d_dst_cap, d_out_len, n);
+        hipLaunchKernelGGL((pcompress_kernel<false, 12>), dim3(grid), dim3(64), 0, stream, d_src, d_src_off,
+                           d_src_len, d_dst, d_dst_off, d_dst_cap, d_out_len, n);
     }
     return (int)hipGetLastError();
 }

@@ -25,6 +25,7 @@ TABLE_U32_HASH5 = 1
 TABLE_AUTO = 2
 PARSE_PARALLEL = 3   # parallel-parse compressor: valid blocks, ratio of LZ4_compress_default
 PARSE_PARALLEL_LARGE = 4   # the same for blocks > 64 KiB
+PARSE_PARALLEL_HQ = 5   # PARSE_PARALLEL with the reference's 13-bit table (ratio of LZ4_compress_default)
 EINVAL = 0x10000
 
 _lock = threading.Lock()
