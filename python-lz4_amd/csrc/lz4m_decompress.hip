@@ -962,7 +962,7 @@ extern "C" int lz4m_decompress_batch_ws(const uint8_t* d_src, const int64_t* d_s
     if (d_work == nullptr || work_bytes < lz4m_decompress_workspace_bytes() || ((uintptr_t)d_work & 7) != 0)
         return LZ4M_EINVAL;
     // LZ4M_SLOW_BATCH: waiting lanes that trigger a general step (tuning)
-    static const int slow_batch = env_int("LZ4M_SLOW_BATCH", 8);
+    static const int slow_batch = env_int("LZ4M_SLOW_BATCH", 6);
     hipError_t e = hipMemsetAsync(d_work, 0, sizeof(unsigned long long), (hipStream_t)stream);
     if (e != hipSuccess) return (int)e;
     hipLaunchKernelGGL(stage_decompress_kernel, dim3((uint32_t)stage_grid(n)), dim3(256), 0, (hipStream_t)stream,
