@@ -23,6 +23,7 @@
 #ifndef LZ4M_H
 #define LZ4M_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -176,6 +177,24 @@ int lz4m_frame_emit(const uint8_t* d_raw, const int64_t* d_raw_off, const int32_
                     const uint8_t* d_cmp, const int64_t* d_cmp_off, const int32_t* d_cmp_len,
                     uint8_t* d_frame, const int64_t* d_frame_off, int block_checksum,
                     int64_t n, lz4m_stream_t stream);
+
+/*
+ * Single-buffer, HOST-pointer functions with the lz4.h contracts, for a C
+ * caller replacing the reference's per-call lz4libs functions one for one
+ * (lz4m_host.hip).  Each copies to the device, runs the batched kernel on a
+ * batch of one and copies back (synchronous; device scratch cached per
+ * thread).  Throughput comes from the batched functions above.
+ *   lz4m_decompress_safe    = LZ4_decompress_safe (lz4.h:191-205)
+ *                             replaces _block.c:357-359 with dict size 0;
+ *   lz4m_compress_default   = LZ4_compress_default (lz4.h:175-189);
+ *   lz4m_compress_block_api = the lz4.block.compress parse (fresh stream,
+ *                             LZ4_compress_fast_continue, _block.c:100-109);
+ *   lz4m_xxh32              = XXH32 (xxhash.h, xxhash.c:392-416).
+ */
+int lz4m_decompress_safe(const char* src, char* dst, int compressedSize, int dstCapacity);
+int lz4m_compress_default(const char* src, char* dst, int srcSize, int dstCapacity);
+int lz4m_compress_block_api(const char* src, char* dst, int srcSize, int dstCapacity, int acceleration);
+uint32_t lz4m_xxh32(const void* input, size_t length, uint32_t seed);
 
 /*
  * Block-record walk of an LZ4 frame already in device memory

@@ -52,6 +52,10 @@ def _declare(lib) -> None:
         "lz4m_frame_block_sizes": ([vp, vp, i32, vp, i64, vp], i32),
         "lz4m_frame_emit": ([vp, vp, vp, vp, vp, vp, vp, vp, i32, i64, vp], i32),
         "lz4m_frame_scan": ([vp, i64, i64, i32, i32, i32, i64, vp, vp, vp, vp, vp], i32),
+        "lz4m_decompress_safe": ([vp, vp, i32, i32], i32),
+        "lz4m_compress_default": ([vp, vp, i32, i32], i32),
+        "lz4m_compress_block_api": ([vp, vp, i32, i32, i32], i32),
+        "lz4m_xxh32": ([vp, C.c_size_t, u32], u32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)

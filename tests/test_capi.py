@@ -21,7 +21,8 @@ def test_header_declares_entry_points():
     for s in ["lz4m_decompress_batch", "lz4m_decompress_batch_dict", "lz4m_decompress_chain",
               "lz4m_compress_batch", "lz4m_xxh32_batch", "lz4m_xxh32_long", "lz4m_compress_bound",
               "lz4m_exclusive_scan", "lz4m_gather", "lz4m_frame_emit", "lz4m_frame_block_sizes",
-              "lz4m_frame_scan"]:
+              "lz4m_frame_scan", "lz4m_decompress_safe", "lz4m_compress_default", "lz4m_compress_block_api",
+              "lz4m_xxh32"]:
         assert s in syms, s
 
 
@@ -42,6 +43,19 @@ def test_compress_bound_and_version():
     assert lib.lz4m_version_number() == 10904
 
 
+def test_header_compiles_as_c():
+    """include/lz4m.h is a plain C header (a cgo / ctypes / C-extension caller
+    includes it): gcc -std=c99 -Wall accepts it."""
+    import subprocess
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "t.c")
+        open(c, "w").write('#include "lz4m.h"\nint main(void) { return LZ4M_TABLE_U16_HASH4; }\n')
+        r = subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.dirname(HEADER), "-c", c, "-o",
+                            os.path.join(d, "t.o")], capture_output=True, text=True)
+        assert r.returncode == 0, r.stderr
+
+
 def test_argument_validation_without_gpu():
     """n == 0 is a no-op and n < 0 is rejected before any HIP call."""
     from lz4 import _native as N
@@ -54,6 +68,10 @@ def test_argument_validation_without_gpu():
     assert lib.lz4m_xxh32_long(None, -1, 0, None, None) == N.EINVAL
     assert lib.lz4m_frame_scan(None, -1, 0, 0, 0, 65536, 1, None, None, None, None, None) == N.EINVAL
     assert lib.lz4m_frame_scan(None, 16, 0, 0, 0, 65536, 1, None, None, None, None, None) == N.EINVAL
+    # host single-buffer functions reject bad sizes before touching a device
+    assert lib.lz4m_decompress_safe(None, None, -1, 10) == -1
+    assert lib.lz4m_compress_default(None, None, -1, 10) == 0
+    assert lib.lz4m_compress_default(None, None, 0x7E000001, 10) == 0
 
 
 def test_no_cpu_fallback():

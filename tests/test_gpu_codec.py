@@ -291,3 +291,33 @@ def test_decompress_kinds_and_sizes(gpu, oracle, kind, block):
     got = gpu_decompress(comp, [block] * n, gpu)
     for (st, out), b in zip(got, blocks):
         assert st == len(b) and out == b
+
+
+def test_host_single_block_functions(gpu, oracle, corpus):
+    """lz4m_decompress_safe / lz4m_compress_default / lz4m_compress_block_api /
+    lz4m_xxh32: host pointers, lz4.h contracts, equal to the oracle."""
+    import ctypes as C
+    lib = N.lib()
+    blocks, ragged = corpus
+    for b in blocks[:6] + ragged:
+        cap = N.compress_bound(len(b))
+        out = C.create_string_buffer(max(cap, 1))
+        n = lib.lz4m_compress_default(b, out, len(b), cap)
+        assert out.raw[:n] == oracle.compress(b), len(b)
+        n2 = lib.lz4m_compress_block_api(b, out, len(b), cap, 1)
+        assert out.raw[:n2] == oracle.compress(b, variant=1), len(b)
+        comp = oracle.compress(b)
+        dec = C.create_string_buffer(max(len(b), 1))
+        assert lib.lz4m_decompress_safe(comp, dec, len(comp), len(b)) == len(b)
+        assert dec.raw[:len(b)] == b
+        assert lib.lz4m_xxh32(b, len(b), 7) == oracle.xxh32(b, 7)
+    # limited output and a corrupt block: the reference's return values
+    b = blocks[0]
+    comp = oracle.compress(b)
+    out = C.create_string_buffer(16)
+    assert lib.lz4m_compress_default(b, out, len(b), 16) == 0
+    dec = C.create_string_buffer(len(b))
+    bad = bytearray(comp)
+    bad[len(bad) // 2] ^= 0xFF
+    assert lib.lz4m_decompress_safe(bytes(bad), dec, len(bad), len(b)) == \
+        oracle.decompress(bytes(bad), len(b))[0]
