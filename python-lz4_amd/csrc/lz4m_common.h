@@ -6,6 +6,16 @@
 namespace lz4m {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+// a byte in LDS (address space 3): LDS and HBM accesses stay distinct
+// instructions (ds_* vs global_*), never merged into generic flat accesses,
+// which the compiler must fence with vmcnt(0) + lgkmcnt(0)
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+__device__ __forceinline__ u32x4 lds_ld16(const lds_u8* p) {
+    u32x4 v;
+    __builtin_memcpy(&v, (const uint8_t*)p, 16);
+    return v;
+}
+__device__ __forceinline__ void lds_st16(lds_u8* p, u32x4 v) { __builtin_memcpy((uint8_t*)p, &v, 16); }
 
 constexpr int kWave = 64;
 
@@ -104,9 +114,13 @@ __device__ __forceinline__ int64_t readlane64(int64_t v, int lane) {
     const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), lane);
     return (int64_t)(((uint64_t)hi << 32) | lo);
 }
+// A lane's global-memory pointer, broadcast.  Rebuilt as a global
+// (address space 1) pointer, so accesses through it stay global_* (not flat).
 template <typename T>
 __device__ __forceinline__ T* readlane_ptr(T* p, int lane) {
-    return reinterpret_cast<T*>(readlane64(reinterpret_cast<int64_t>(p), lane));
+    typedef __attribute__((address_space(1))) T gT;
+    gT* g = (gT*)(uintptr_t)readlane64(reinterpret_cast<int64_t>(p), lane);
+    return (T*)g;
 }
 
 }  // namespace lz4m

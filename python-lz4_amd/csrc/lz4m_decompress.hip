@@ -53,9 +53,9 @@ struct Lane {
     // STAGE mode (the hot kernel): an LDS output stage holding output bytes
     // [F - 16, op) at offset p - F + 16 ([0, F) is in HBM, F % 64 == 0) and
     // an LDS input window holding compressed bytes [ib, ib + 64).
-    uint8_t* stage;
+    lds_u8* stage;
     int64_t F;
-    uint8_t* win;
+    lds_u8* win;
     int64_t ib;
 };
 
@@ -80,20 +80,21 @@ struct Lane {
 constexpr int kStage = 96;
 constexpr int kWin = 64;
 
-__device__ __forceinline__ uint8_t* stage_at(const Lane& L, int64_t p) { return L.stage + (p - L.F + 16); }
+__device__ __forceinline__ lds_u8* stage_at(const Lane& L, int64_t p) { return L.stage + (p - L.F + 16); }
 
 // Chunk [F, F + 64) is final: write it to HBM and rebase the stage by 64
 // (the 32 bytes [F + 48, F + 80) move to the front).
 __device__ __forceinline__ void stage_flush(Lane& L) {
-    const u32x4 a = ld16(L.stage + 16), b = ld16(L.stage + 32), c = ld16(L.stage + 48), d = ld16(L.stage + 64);
-    const u32x4 e = ld16(L.stage + 80);
+    const u32x4 a = lds_ld16(L.stage + 16), b = lds_ld16(L.stage + 32), c = lds_ld16(L.stage + 48),
+                d = lds_ld16(L.stage + 64);
+    const u32x4 e = lds_ld16(L.stage + 80);
     uint8_t* o = L.dst + L.F;
     st16(o, a);
     st16(o + 16, b);
     st16(o + 32, c);
     st16(o + 48, d);
-    st16(L.stage, d);
-    st16(L.stage + 16, e);
+    lds_st16(L.stage, d);
+    lds_st16(L.stage + 16, e);
     L.F += 64;
 }
 
@@ -106,7 +107,8 @@ __device__ __forceinline__ void stage_sync(Lane& L, int64_t p) {
 // 16 output bytes from q, a match source: the stage if q >= F - 16, else
 // HBM (then q + 16 <= F: already flushed).
 __device__ __forceinline__ u32x4 out_read16(const Lane& L, int64_t q) {
-    return q >= L.F - 16 ? ld16(stage_at(L, q)) : ld16(L.dst + q);
+    if (q >= L.F - 16) return lds_ld16(stage_at(L, q));
+    return ld16(L.dst + q);
 }
 
 // Store exactly k (0..16) bytes of v at p (any alignment).
@@ -154,7 +156,7 @@ template <bool STAGE>
 __device__ __forceinline__ u32x4 in16(const Lane& L, int64_t p) {
     if (STAGE) {
         const int64_t d = p - L.ib;
-        if (d >= 0 && d <= kWin - 16) return ld16(L.win + d);
+        if (d >= 0 && d <= kWin - 16) return lds_ld16(L.win + d);
     }
     return ld16_guarded(L.src + p, L.iend - p);
 }
@@ -168,7 +170,7 @@ __device__ __forceinline__ uint32_t in_le16(const Lane& L, int64_t p) {
 __device__ __forceinline__ void stage_literal(Lane& L, int64_t op, int64_t ip, int64_t len) {
     for (int64_t i = 0; i < len; i += 16) {
         stage_sync(L, op + i);
-        st16(stage_at(L, op + i), in16<true>(L, ip + i));
+        lds_st16(stage_at(L, op + i), in16<true>(L, ip + i));
     }
 }
 
@@ -177,7 +179,7 @@ __device__ __forceinline__ void stage_match(Lane& L, int64_t op, int64_t off, in
     if (off >= 16) {
         for (int64_t i = 0; i < len; i += 16) {
             stage_sync(L, op + i);
-            st16(stage_at(L, op + i), out_read16(L, op + i - off));
+            lds_st16(stage_at(L, op + i), out_read16(L, op + i - off));
         }
         return;
     }
@@ -193,7 +195,7 @@ __device__ __forceinline__ void stage_match(Lane& L, int64_t op, int64_t off, in
     }
     for (int64_t i = 0; i < len; i += step) {
         stage_sync(L, op + i);
-        st16(stage_at(L, op + i), pat);
+        lds_st16(stage_at(L, op + i), pat);
     }
 }
 
@@ -201,7 +203,7 @@ __device__ __forceinline__ void stage_match(Lane& L, int64_t op, int64_t off, in
 __device__ __forceinline__ void stage_finish(Lane& L, int64_t end) {
     while (L.F + 64 <= end) stage_flush(L);
     for (int64_t p = L.F; p < end; p += 16) {
-        put_exact(L.dst + p, ld16(stage_at(L, p)), (uint32_t)(end - p < 16 ? end - p : 16));
+        put_exact(L.dst + p, lds_ld16(stage_at(L, p)), (uint32_t)(end - p < 16 ? end - p : 16));
     }
 }
 
@@ -210,7 +212,7 @@ __device__ __forceinline__ void stage_finish(Lane& L, int64_t end) {
 __device__ __forceinline__ void stage_reload(Lane& L, int64_t E) {
     L.F = E & ~(int64_t)63;
     for (int64_t x = L.F - 16; x < E; x += 16) {
-        if (x >= 0) st16(stage_at(L, x), ld16_guarded(L.dst + x, L.oend - x));
+        if (x >= 0) lds_st16(stage_at(L, x), ld16_guarded(L.dst + x, L.oend - x));
     }
 }
 
@@ -223,8 +225,8 @@ __device__ __forceinline__ void win_sync(Lane& L) {
     const int64_t first = shift ? nb + 32 : nb;
     u32x4 k0 = u32x4{0, 0, 0, 0}, k1 = k0;
     if (shift) {
-        k0 = ld16(L.win + 32);
-        k1 = ld16(L.win + 48);
+        k0 = lds_ld16(L.win + 32);
+        k1 = lds_ld16(L.win + 48);
     }
     u32x4 v[4];
 #pragma unroll
@@ -234,12 +236,12 @@ __device__ __forceinline__ void win_sync(Lane& L) {
         if (x >= first) v[k] = x + 16 <= L.iend ? ld16(L.src + x) : ld16_guarded(L.src + x, L.iend - x);
     }
     if (shift) {
-        st16(L.win, k0);
-        st16(L.win + 16, k1);
+        lds_st16(L.win, k0);
+        lds_st16(L.win + 16, k1);
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        if (nb + 16 * k >= first) st16(L.win + 16 * k, v[k]);
+        if (nb + 16 * k >= first) lds_st16(L.win + 16 * k, v[k]);
     }
     L.ib = nb;
 }
@@ -397,7 +399,7 @@ template <bool STAGE>
 __device__ __forceinline__ void window_literal(Lane& L, int64_t op, u32x4 w, int64_t lit) {
     if (STAGE) {
         stage_sync(L, op);
-        st16(stage_at(L, op), window_shift1(w));   // wild 16-byte store
+        lds_st16(stage_at(L, op), window_shift1(w));   // wild 16-byte store
     } else {
         st16(L.dst + op, window_shift1(w));   // wild 16-byte store, inside the oend-32 margin
     }
@@ -720,11 +722,11 @@ __device__ __forceinline__ bool fast_seq(const Lane& L, u32x4 w, FastSeq& f) {
 }
 
 __device__ __forceinline__ void fast_exec(Lane& L, u32x4 w, const FastSeq& f) {
-    st16(stage_at(L, L.op), window_shift1(w));   // literals (wild), op < F + 64
+    lds_st16(stage_at(L, L.op), window_shift1(w));   // literals (wild), op < F + 64
     const int64_t opm = L.op + f.lit;
     for (int64_t i = 0; i < f.ml; i += 16) {
         stage_sync(L, opm + i);
-        st16(stage_at(L, opm + i), out_read16(L, opm + i - f.off));
+        lds_st16(stage_at(L, opm + i), out_read16(L, opm + i - f.off));
     }
     L.ip = f.ipn;
     L.op = opm + f.ml;
@@ -751,8 +753,8 @@ __global__ __launch_bounds__(256, 4) void stage_decompress_kernel(const uint8_t*
     Lane L;
     L.live = false;
     L.result = -1;
-    L.stage = stages + threadIdx.x * kStage;
-    L.win = wins + threadIdx.x * kWin;
+    L.stage = (lds_u8*)(stages + threadIdx.x * kStage);
+    L.win = (lds_u8*)(wins + threadIdx.x * kWin);
     L.ip = 0;
     L.op = 0;
     L.F = 0;
@@ -808,7 +810,7 @@ __global__ __launch_bounds__(256, 4) void stage_decompress_kernel(const uint8_t*
         if (L.live) {
             win_sync(L);
             stage_sync(L, L.op);
-            w = ld16(L.win + (L.ip - L.ib));
+            w = lds_ld16(L.win + (L.ip - L.ib));
             fok = fast_seq(L, w, f);
         }
         const uint64_t fm = __ballot(fok);
