@@ -5,6 +5,7 @@ from ._block import (  # noqa: F401  batched / device-resident extensions
     decompress_many,
     compress_batch,
     decompress_batch,
+    decompress_host,
     compact,
     xxh32_batch,
     HC_LEVEL_MIN,

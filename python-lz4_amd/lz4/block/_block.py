@@ -328,3 +328,69 @@ def xxh32_batch(src: torch.Tensor, off: torch.Tensor, length: torch.Tensor, seed
     out = torch.empty(n, dtype=torch.int32, device=src.device)
     N.launch_xxh32_batch(src, off, length.to(torch.int64), seed, out, n, stream)
     return out
+
+
+def decompress_host(comp: torch.Tensor, comp_off: torch.Tensor, comp_len: torch.Tensor, out: torch.Tensor,
+                    out_off: torch.Tensor, out_cap: torch.Tensor, *, chunk_blocks: int = 65536,
+                    device=None) -> torch.Tensor:
+    """Decode n blocks that start and end in HOST memory (a file's or
+    socket's bytes), pipelined over PCIe: chunk i+1 is copied in while
+    chunk i decodes and chunk i-1 is copied out (three HIP streams, two
+    device buffer sets).  comp / out are uint8 host tensors (pin them for
+    the copies to overlap); comp_off / out_off int64, comp_len / out_cap
+    int32 host tensors, blocks in increasing position order in both.
+    Returns the int32 status of every block (host), as LZ4_decompress_safe
+    would return it.  A chunk needs >= 64 K blocks to keep the decoder busy
+    (a 64 KiB block takes one lane ~34 ms)."""
+    dev = device or N.device()
+    n = comp_off.numel()
+    status = torch.empty(n, dtype=torch.int32, device=dev)
+    if n == 0:
+        return status.cpu()
+    c_off, c_len = comp_off.to(torch.int64), comp_len.to(torch.int32)
+    o_off, o_cap = out_off.to(torch.int64), out_cap.to(torch.int32)
+    if bool((c_off[1:] < c_off[:-1] + c_len[:-1]).any()) or bool((o_off[1:] < o_off[:-1] + o_cap[:-1]).any()):
+        raise ValueError("blocks must be in increasing, non-overlapping position order")
+    chunks = [(lo, min(n, lo + chunk_blocks)) for lo in range(0, n, chunk_blocks)]
+
+    def span(off, ln, lo, hi):
+        return int(off[lo]), int(off[hi - 1]) + int(ln[hi - 1])
+
+    in_max = max(b - a for a, b in (span(c_off, c_len, lo, hi) for lo, hi in chunks))
+    out_max = max(b - a for a, b in (span(o_off, o_cap, lo, hi) for lo, hi in chunks))
+    d_in = [torch.empty(in_max + 16, dtype=torch.uint8, device=dev) for _ in range(2)]
+    d_out = [torch.empty(max(out_max, 1), dtype=torch.uint8, device=dev) for _ in range(2)]
+    s_in, s_dec, s_out = torch.cuda.Stream(dev), torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    ev_in = [torch.cuda.Event() for _ in range(2)]
+    ev_dec = [torch.cuda.Event() for _ in range(2)]
+    ev_free = [None, None]
+    cur = torch.cuda.current_stream(dev)
+    s_in.wait_stream(cur)
+    for i, (lo, hi) in enumerate(chunks):
+        b = i & 1
+        a0, a1 = span(c_off, c_len, lo, hi)
+        b0, b1 = span(o_off, o_cap, lo, hi)
+        with torch.cuda.stream(s_in):
+            if ev_free[b] is not None:
+                s_in.wait_event(ev_free[b])                    # chunk i-2 has left buffer b
+            d_in[b][: a1 - a0].copy_(comp[a0:a1], non_blocking=True)
+            meta = torch.stack([c_off[lo:hi] - a0, o_off[lo:hi] - b0]).to(dev, non_blocking=True)
+            lens = torch.stack([c_len[lo:hi], o_cap[lo:hi]]).to(dev, non_blocking=True)
+            ev_in[b].record(s_in)
+        with torch.cuda.stream(s_dec):
+            s_dec.wait_event(ev_in[b])
+            N.launch_decompress(d_in[b], meta[0], lens[0], d_out[b], meta[1], lens[1], status[lo:hi], hi - lo,
+                                s_dec)
+            meta.record_stream(s_dec)
+            lens.record_stream(s_dec)
+            ev_dec[b].record(s_dec)
+        with torch.cuda.stream(s_out):
+            s_out.wait_event(ev_dec[b])
+            out[b0:b1].copy_(d_out[b][: b1 - b0], non_blocking=True)
+            ev_free[b] = torch.cuda.Event()
+            ev_free[b].record(s_out)
+    cur.wait_stream(s_out)
+    cur.wait_stream(s_dec)
+    st = status.cpu()
+    torch.cuda.synchronize(dev)
+    return st

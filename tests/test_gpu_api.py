@@ -363,3 +363,30 @@ def test_frame_device_roundtrip_large_blocks(gpu):
                                       content_checksum=True, parse=parse)
         out = lz4.frame.decompress_device(f)
         assert torch.equal(out, d)
+
+
+def test_decompress_host_pipelined(gpu):
+    """lz4.block.decompress_host: host-resident compressed blocks decoded in
+    pipelined chunks into host memory; statuses and bytes equal the
+    reference decoder's."""
+    import torch
+    import oracle as O
+    from lz4 import _synth
+    raw = _synth.blocks(40, "silesia", seed=21)
+    blocks = [raw[i].tobytes()[: 65536 - 97 * (i % 5)] for i in range(len(raw))]
+    orc = O.Oracle()
+    comp = [orc.compress(b) for b in blocks]
+    comp[7] = comp[7][:-3]                         # a truncated block
+    packed = torch.frombuffer(bytearray(b"".join(comp)), dtype=torch.uint8).pin_memory()
+    lens = torch.tensor([len(c) for c in comp], dtype=torch.int32)
+    offs = torch.cumsum(lens.to(torch.int64), 0) - lens.to(torch.int64)
+    caps = torch.tensor([len(b) for b in blocks], dtype=torch.int32)
+    ooff = torch.cumsum(caps.to(torch.int64), 0) - caps.to(torch.int64)
+    out = torch.zeros(int(caps.sum()), dtype=torch.uint8).pin_memory()
+    st = lz4.block.decompress_host(packed, offs, lens, out, ooff, caps, chunk_blocks=9)
+    for i, (c, b) in enumerate(zip(comp, blocks)):
+        want, data = orc.decompress(c, len(b))
+        assert int(st[i]) == want, i
+        if want >= 0:
+            o = int(ooff[i])
+            assert out[o:o + want].numpy().tobytes() == data[:want], i
