@@ -309,6 +309,16 @@ def main():
         extra["decompress_random_kernel_gbs"] = round((r_cbytes + nr * BLOCK) / r_ev / 1e9, 1)
         del rsrc, rdst, r_slots, rst
 
+    # ---- extra: measured HBM copy bandwidth (report the spec and a copy) ----
+    cb = 8 << 30
+    ca = torch.empty(cb, dtype=torch.uint8, device=dev)
+    cbuf = torch.empty(cb, dtype=torch.uint8, device=dev)
+    c_wall, c_ev = time_kernel(lambda: cbuf.copy_(ca), 3, 1, world)
+    extra["hbm_copy_gb_s"] = round(2 * cb / c_ev / 1e9, 1)
+    extra["hbm_copy_note"] = "device-to-device copy of 8 GiB (read + write bytes / time), torch copy_"
+    del ca, cbuf
+    torch.cuda.empty_cache()
+
     log("[bench] decode done")
     # ---- extra: config 4, one frame of 4 MiB independent blocks + XXH32 content checksum ----
     if args.frame_gib > 0:
@@ -389,6 +399,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic},
         "decompress_kernel_ms": round(d_ev * 1e3, 3),
+        "decompress_read_gbs": round(comp_total / d_ev / 1e9, 1),
         "compress": c3,
         "extra": extra,
     }

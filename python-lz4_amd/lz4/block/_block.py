@@ -364,8 +364,18 @@ def decompress_host(comp: torch.Tensor, comp_off: torch.Tensor, comp_len: torch.
     ev_in = [torch.cuda.Event() for _ in range(2)]
     ev_dec = [torch.cuda.Event() for _ in range(2)]
     ev_free = [None, None]
+    # every chunk's block offsets, rebased to its buffers, in one upload (a
+    # per-chunk upload from pageable memory would block the host thread)
+    base_c = torch.zeros(n, dtype=torch.int64)
+    base_o = torch.zeros(n, dtype=torch.int64)
+    for lo, hi in chunks:
+        base_c[lo:hi] = int(c_off[lo])
+        base_o[lo:hi] = int(o_off[lo])
+    meta = torch.stack([c_off - base_c, o_off - base_o]).to(dev)
+    lens = torch.stack([c_len, o_cap]).to(dev)
     cur = torch.cuda.current_stream(dev)
     s_in.wait_stream(cur)
+    s_out.wait_stream(cur)
     for i, (lo, hi) in enumerate(chunks):
         b = i & 1
         a0, a1 = span(c_off, c_len, lo, hi)
@@ -374,15 +384,11 @@ def decompress_host(comp: torch.Tensor, comp_off: torch.Tensor, comp_len: torch.
             if ev_free[b] is not None:
                 s_in.wait_event(ev_free[b])                    # chunk i-2 has left buffer b
             d_in[b][: a1 - a0].copy_(comp[a0:a1], non_blocking=True)
-            meta = torch.stack([c_off[lo:hi] - a0, o_off[lo:hi] - b0]).to(dev, non_blocking=True)
-            lens = torch.stack([c_len[lo:hi], o_cap[lo:hi]]).to(dev, non_blocking=True)
             ev_in[b].record(s_in)
         with torch.cuda.stream(s_dec):
             s_dec.wait_event(ev_in[b])
-            N.launch_decompress(d_in[b], meta[0], lens[0], d_out[b], meta[1], lens[1], status[lo:hi], hi - lo,
-                                s_dec)
-            meta.record_stream(s_dec)
-            lens.record_stream(s_dec)
+            N.launch_decompress(d_in[b], meta[0, lo:hi], lens[0, lo:hi], d_out[b], meta[1, lo:hi], lens[1, lo:hi],
+                                status[lo:hi], hi - lo, s_dec)
             ev_dec[b].record(s_dec)
         with torch.cuda.stream(s_out):
             s_out.wait_event(ev_dec[b])
