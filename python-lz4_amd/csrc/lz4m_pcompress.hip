@@ -117,6 +117,23 @@ __device__ __forceinline__ uint32_t wave_sort(uint32_t key, uint32_t lane) {
 
 __device__ __forceinline__ int32_t ext_len(int32_t x) { return x >= 15 ? 1 + (x - 15) / 255 : 0; }
 
+// inclusive prefix sum across the wave: row_shr 1/2/4/8 inside 16-lane rows,
+// then row_bcast:15 / row_bcast:31 carry the row totals (VALU only)
+__device__ __forceinline__ int32_t wave_incl_sum(int32_t v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);   // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);   // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);   // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);   // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);   // row_bcast:15 -> rows 1, 3
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);   // row_bcast:31 -> rows 2, 3
+    return v;
+}
+
+// set bits of m in lanes below this one
+__device__ __forceinline__ int32_t count_below(uint64_t m) {
+    return (int32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
 // Wave-cooperative forward match length of s[a..] vs s[c..] (c < a), at most
 // `lim` bytes; a + lim <= n - 5, so every 4-byte read stays in the block.
 __device__ __forceinline__ int32_t wave_count(const uint8_t* s, int32_t a, int32_t c, int32_t lim, uint32_t lane) {
@@ -161,9 +178,14 @@ __device__ __forceinline__ int32_t emit_seqs(const uint8_t* s, uint8_t* d, int32
     if (op + total > cap) return -1;
     for (int32_t t0 = 0; t0 < ptotal; t0 += 64) {
         const int32_t t = t0 + (int32_t)lane;
+        // last sequence k < ns with pbase_k <= t (pbase ascends with k)
         int sq = 0;
-        for (int k = 1; k < ns; ++k)
-            if (t >= rdl(pbase, k)) sq = k;
+#pragma unroll
+        for (int step = 32; step > 0; step >>= 1) {
+            const int k = sq + step;
+            const int32_t pk = __shfl(pbase, k < ns ? k : 0);
+            if (k < ns && pk <= t) sq = k;
+        }
         const int32_t pb = __shfl(pbase, sq), ob = __shfl(obase, sq), L = __shfl(lit, sq), O = __shfl(off, sq),
                       M = __shfl(ml, sq), S = __shfl(lstart, sq);
         const int32_t EL = ext_len(L);
@@ -198,9 +220,9 @@ __device__ __forceinline__ int32_t emit_seqs(const uint8_t* s, uint8_t* d, int32
         }
     }
     // long literals: coalesced 16-byte-per-lane copies
-    for (int k = 0; k < ns; ++k) {
+    for (uint64_t lm = __ballot((int)lane < ns && lit >= kLongLit); lm; lm &= lm - 1) {
+        const int k = __builtin_ctzll(lm);
         const int32_t L = rdl(lit, k);
-        if (L < kLongLit) continue;
         const int32_t S = rdl(lstart, k);
         uint8_t* o = d + op + rdl(obase, k) + 1 + ext_len(L);
         for (int32_t x = 16 * (int32_t)lane; x < L; x += 16 * 64) {
@@ -326,45 +348,64 @@ __global__ __launch_bounds__(64) void pcompress_kernel(const uint8_t* __restrict
             Chunk B;
             if (has_next)
                 chunk_issue<BIG, HB>(B, s, table, p0 + 64, load_word(s, p0 + 64 + (int32_t)lane, N), N, mlast, lane);
-            // ---- greedy parse of chunk p0
-            int ns = 0;
-            int32_t q_ls = 0, q_lit = 0, q_off = 0, q_ml = 0, q_ob = 0, q_pb = 0;   // sequence ns in lane ns
-            int32_t acc = 0, pacc = 0;
+            // ---- greedy parse of chunk p0.  The serial walk only picks the
+            // sequence starts: the first verified lane at or after the previous
+            // match's end (catch-up moves a start back but not the end).
+            uint64_t chosen = 0;
+            int32_t Lx = L;   // match length, extended past 20 for the picked lanes
             while (cur < p0 + 64 && cur <= mlast) {
                 const int32_t rel = cur - p0;
                 const uint64_t m = rel <= 0 ? mask : (mask >> rel) << rel;
                 if (m == 0) break;
                 const int j = __builtin_ctzll(m);
-                int32_t st = p0 + j;
-                int32_t c = rdl(A.cand, j);
+                const int32_t st = p0 + j;
                 int32_t len = rdl(L, j);
-                int32_t bk = rdl(back, j);
                 const int32_t lim = matchlimit - st;
-                if (len == 20 && len < lim) len = 20 + wave_count(s, st + 20, c + 20, lim - 20, lane);
-                // catch-up over pending literals (lz4.c:1080)
-                if (bk > st - anchor) bk = st - anchor;
-                if (bk == 4) {
-                    while (st - bk > anchor && c - bk > 0 && s[st - bk - 1] == s[c - bk - 1]) ++bk;
+                if (len == 20 && len < lim) {
+                    len = 20 + wave_count(s, st + 20, rdl(A.cand, j) + 20, lim - 20, lane);
+                    if ((int)lane == j) Lx = len;
+                }
+                chosen |= 1ull << j;
+                cur = st + len;
+            }
+            const int ns = __builtin_popcountll(chosen);
+            int32_t q_ls = 0, q_lit = 0, q_off = 0, q_ml = 0, q_ob = 0, q_pb = 0;   // sequence k in lane k
+            int32_t acc = 0, pacc = 0;
+            if (ns > 0) {
+                // every picked lane at once: its anchor is the previous picked
+                // lane's match end (or the carried anchor), then catch-up over
+                // the pending literals (lz4.c:1080), sizes, prefix sums, and a
+                // compaction of sequence k into lane k
+                const bool isch = (chosen >> lane) & 1u;
+                const uint64_t below = chosen & (lane ? (~0ull >> (64 - lane)) : 0ull);
+                const int32_t p = p0 + (int32_t)lane;
+                const int prevl = below ? 63 - __builtin_clzll(below) : 0;
+                const int32_t pend = __shfl(p + Lx, prevl);
+                const int32_t anc = below ? pend : anchor;
+                int32_t st = p, c = A.cand, len = Lx, bk = back;
+                if (isch) {
+                    if (bk > st - anc) bk = st - anc;
+                    if (bk == 4) {
+                        while (st - bk > anc && c - bk > 0 && s[st - bk - 1] == s[c - bk - 1]) ++bk;
+                    }
                 }
                 st -= bk;
                 c -= bk;
                 len += bk;
-                const int32_t lit = st - anchor;
-                if ((int)lane == ns) {
-                    q_ls = anchor;
-                    q_lit = lit;
-                    q_off = st - c;
-                    q_ml = len;
-                    q_ob = acc;
-                    q_pb = pacc;
-                }
-                const int32_t sz = seq_size(lit, len);
-                acc += sz;
-                pacc += lit >= kLongLit ? sz - lit : sz;
-                ++ns;
-                cur = st + len;
+                const int32_t lit = st - anc;
+                const int32_t sz = isch ? seq_size(lit, len) : 0;
+                const int32_t psz = isch ? (lit >= kLongLit ? sz - lit : sz) : 0;
+                const int32_t isz = wave_incl_sum(sz), ipsz = wave_incl_sum(psz);
+                acc = rdl(isz, 63);
+                pacc = rdl(ipsz, 63);
+                const int addr = (isch ? count_below(chosen) : 63) << 2;
+                q_ls = __builtin_amdgcn_ds_permute(addr, anc);
+                q_lit = __builtin_amdgcn_ds_permute(addr, lit);
+                q_off = __builtin_amdgcn_ds_permute(addr, st - c);
+                q_ml = __builtin_amdgcn_ds_permute(addr, len);
+                q_ob = __builtin_amdgcn_ds_permute(addr, isz - sz);
+                q_pb = __builtin_amdgcn_ds_permute(addr, ipsz - psz);
                 anchor = cur;
-                if (ns == 64) break;
             }
             if (ns > 0) {
                 const int32_t w = emit_seqs(s, d, op, cap, ns, q_ls, q_lit, q_off, q_ml, q_ob, q_pb, acc, pacc, p0,

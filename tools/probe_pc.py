@@ -29,12 +29,15 @@ for kind in kinds:
         torch.cuda.synchronize()
         ts.append(time.perf_counter() - t)
     par = int(olen.to(torch.int64).sum())
+    import hashlib
+    sizes_digest = hashlib.sha1(olen.cpu().numpy().tobytes()).hexdigest()[:12]
     dst = torch.empty(n * 65536, dtype=torch.uint8, device=dev)
     st = torch.empty(n, dtype=torch.int32, device=dev)
     N.launch_decompress(slots, soff, olen, dst, so, sl, st, n)
     ok = bool((st == 65536).all()) and torch.equal(dst, src)
     print(f"{kind}: parallel {n * 65536 / min(ts) / 2**30:.2f} GiB/s, ratio {n * 65536 / par:.4f} "
-          f"(exact {n * 65536 / exact:.4f}, {par / exact - 1:+.2%} size), round trip {'ok' if ok else 'FAILED'}",
+          f"(exact {n * 65536 / exact:.4f}, {par / exact - 1:+.2%} size), round trip {'ok' if ok else 'FAILED'}, "
+          f"sizes {sizes_digest}",
           flush=True)
     del src, slots, dst
     torch.cuda.empty_cache()
