@@ -55,9 +55,9 @@ __device__ __forceinline__ uint32_t eq_prefix16(u32x4 a, u32x4 b) {
 
 __device__ __forceinline__ int32_t rdl(int32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
 
-// v of lane (lane ^ j), j a power of two, without the LDS crossbar: DPP
-// within 16-lane rows (quad_perm, row_shl/shr, row_ror), gfx950 permlane
-// swaps across rows and halves.
+// v of lane (lane ^ j), j a power of two: DPP within 16-lane rows
+// (quad_perm, row_ror), ds_swizzle for 4 and 16 (the LDS pipe, which this
+// VALU-bound kernel leaves idle), the gfx950 permlane swap across halves.
 template <int J>
 __device__ __forceinline__ uint32_t xor_lane(uint32_t v, uint32_t lane) {
     const int x = (int)v;
@@ -66,14 +66,13 @@ __device__ __forceinline__ uint32_t xor_lane(uint32_t v, uint32_t lane) {
     } else if constexpr (J == 2) {
         return (uint32_t)__builtin_amdgcn_mov_dpp(x, 0x4E, 0xF, 0xF, false);   // quad_perm:[2,3,0,1]
     } else if constexpr (J == 4) {
-        const int up = __builtin_amdgcn_update_dpp(x, x, 0x104, 0xF, 0xF, false);   // row_shl:4: lane + 4
-        const int dn = __builtin_amdgcn_update_dpp(x, x, 0x114, 0xF, 0xF, false);   // row_shr:4: lane - 4
-        return (uint32_t)((lane & 4) ? dn : up);
+        // ds_swizzle bit mode (and 0x1F, xor 4): one LDS-pipe instruction
+        // instead of two DPP moves and a select on the VALU
+        return (uint32_t)__builtin_amdgcn_ds_swizzle(x, 0x101F);
     } else if constexpr (J == 8) {
         return (uint32_t)__builtin_amdgcn_mov_dpp(x, 0x128, 0xF, 0xF, false);   // row_ror:8
     } else if constexpr (J == 16) {
-        const auto p = __builtin_amdgcn_permlane16_swap((unsigned)x, (unsigned)x, false, false);
-        return (lane & 16) ? p[0] : p[1];
+        return (uint32_t)__builtin_amdgcn_ds_swizzle(x, 0x401F);   // xor 16 within 32 lanes
     } else {
         const auto p = __builtin_amdgcn_permlane32_swap((unsigned)x, (unsigned)x, false, false);
         return (lane & 32) ? p[0] : p[1];
@@ -351,22 +350,24 @@ __global__ __launch_bounds__(64) void pcompress_kernel(const uint8_t* __restrict
             // ---- greedy parse of chunk p0.  The serial walk only picks the
             // sequence starts: the first verified lane at or after the previous
             // match's end (catch-up moves a start back but not the end).
+            // (verified lanes all start at or before mlast, so `rem` -- the
+            // verified lanes at or after the walk position -- running empty
+            // ends the walk)
             uint64_t chosen = 0;
             int32_t Lx = L;   // match length, extended past 20 for the picked lanes
-            while (cur < p0 + 64 && cur <= mlast) {
-                const int32_t rel = cur - p0;
-                const uint64_t m = rel <= 0 ? mask : (mask >> rel) << rel;
-                if (m == 0) break;
-                const int j = __builtin_ctzll(m);
-                const int32_t st = p0 + j;
+            const int32_t rel0 = cur - p0;
+            uint64_t rem = rel0 <= 0 ? mask : rel0 >= 64 ? 0ull : mask & (~0ull << rel0);
+            while (rem) {
+                const int j = __builtin_ctzll(rem);
                 int32_t len = rdl(L, j);
-                const int32_t lim = matchlimit - st;
-                if (len == 20 && len < lim) {
-                    len = 20 + wave_count(s, st + 20, rdl(A.cand, j) + 20, lim - 20, lane);
+                if (len == 20 && len < matchlimit - (p0 + j)) {
+                    len = 20 + wave_count(s, p0 + j + 20, rdl(A.cand, j) + 20, matchlimit - (p0 + j) - 20, lane);
                     if ((int)lane == j) Lx = len;
                 }
                 chosen |= 1ull << j;
-                cur = st + len;
+                const int32_t e = j + len;   // match end, relative to p0
+                cur = p0 + e;
+                rem = e >= 64 ? 0ull : rem & (~0ull << e);
             }
             const int ns = __builtin_popcountll(chosen);
             int32_t q_ls = 0, q_lit = 0, q_off = 0, q_ml = 0, q_ob = 0, q_pb = 0;   // sequence k in lane k
