@@ -16,17 +16,23 @@
 //
 // Mapping: one wavefront per block (<= 64 KiB, u16 positions in a 16 KiB LDS
 // table), 64 consecutive positions per step:
-//   1. each lane hashes its position; a 64-key bitonic sort of (hash, lane)
-//      gives the nearest earlier lane with the same hash and whether a later
-//      lane shares it -- so candidates are exactly "most recent previous
-//      occurrence" and the table is updated by one writer per hash;
+//   1. each lane hashes its position; one wave ballot per hash bit gives the
+//      mask of lanes sharing its hash, hence the nearest earlier lane with
+//      the same hash and whether a later lane shares it -- so candidates are
+//      exactly "most recent previous occurrence" and the table is updated by
+//      one writer per hash;
 //   2. every lane verifies its candidate and measures forward (<= 20 B) and
 //      backward (<= 4 B) match bytes in parallel: one memory round trip per
 //      step, not per sequence;
-//   3. the greedy parse walks the ballot mask of verified lanes (scalar);
-//   4. the step's sequences are encoded byte-parallel: sizes, a wave prefix
-//      sum, then lane t computes output byte t (token, length bytes, literal,
-//      offset) -- one coalesced 64-byte store per round.
+//   3. the greedy walk over the ballot mask of verified lanes (scalar) only
+//      picks the sequence starts; anchors, catch-up, sizes, prefix sums and
+//      the compaction of sequence k into lane k run across the wave;
+//   4. the step's sequences are encoded byte-parallel: lane t computes output
+//      byte t (token, length bytes, literal, offset) -- one coalesced 64-byte
+//      store per round.
+// The kernel is bound by instruction issue (VALU ~0.75 per CU-cycle, PMC):
+// every step above is written to keep both the VALU and the per-CU scalar
+// unit short.
 #include "lz4m_common.h"
 #include "../../include/lz4m.h"
 
@@ -55,63 +61,22 @@ __device__ __forceinline__ uint32_t eq_prefix16(u32x4 a, u32x4 b) {
 
 __device__ __forceinline__ int32_t rdl(int32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
 
-// v of lane (lane ^ j), j a power of two: DPP within 16-lane rows
-// (quad_perm, row_ror), ds_swizzle for 4 and 16 (the LDS pipe, which this
-// VALU-bound kernel leaves idle), the gfx950 permlane swap across halves.
-template <int J>
-__device__ __forceinline__ uint32_t xor_lane(uint32_t v, uint32_t lane) {
-    const int x = (int)v;
-    if constexpr (J == 1) {
-        return (uint32_t)__builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, false);   // quad_perm:[1,0,3,2]
-    } else if constexpr (J == 2) {
-        return (uint32_t)__builtin_amdgcn_mov_dpp(x, 0x4E, 0xF, 0xF, false);   // quad_perm:[2,3,0,1]
-    } else if constexpr (J == 4) {
-        // ds_swizzle bit mode (and 0x1F, xor 4): one LDS-pipe instruction
-        // instead of two DPP moves and a select on the VALU
-        return (uint32_t)__builtin_amdgcn_ds_swizzle(x, 0x101F);
-    } else if constexpr (J == 8) {
-        return (uint32_t)__builtin_amdgcn_mov_dpp(x, 0x128, 0xF, 0xF, false);   // row_ror:8
-    } else if constexpr (J == 16) {
-        return (uint32_t)__builtin_amdgcn_ds_swizzle(x, 0x401F);   // xor 16 within 32 lanes
-    } else {
-        const auto p = __builtin_amdgcn_permlane32_swap((unsigned)x, (unsigned)x, false, false);
-        return (lane & 32) ? p[0] : p[1];
+// Mask of the lanes whose HB-bit hash equals this lane's (active lanes only):
+// AND over the hash bits of "same bit" masks, each from one wave ballot.
+template <int HB>
+__device__ __forceinline__ uint64_t same_hash_mask(uint32_t h, bool act) {
+    const uint64_t a = __ballot(act);
+    uint32_t lo = (uint32_t)a, hi = (uint32_t)(a >> 32);
+#pragma unroll
+    for (int b = 0; b < HB; ++b) {
+        const uint32_t rep = (uint32_t)((int32_t)(h << (31 - b)) >> 31);   // bit b, replicated
+        const uint64_t B = __ballot(rep != 0u);
+        // mask &= ~(B ^ rep) as one v_bitop3 per half: f(S0, S1, S2) =
+        // S1 & (S0 xnor S2), truth table 0x84 (symmetric in S0 / S2)
+        lo = __builtin_amdgcn_bitop3_b32((uint32_t)B, lo, rep, 0x84);
+        hi = __builtin_amdgcn_bitop3_b32((uint32_t)(B >> 32), hi, rep, 0x84);
     }
-}
-
-// one bitonic compare-exchange stage (block size K, distance J)
-template <int K, int J>
-__device__ __forceinline__ uint32_t bitonic_stage(uint32_t key, uint32_t lane) {
-    const uint32_t other = xor_lane<J>(key, lane);
-    const bool up = (lane & K) == 0;
-    const bool lower = (lane & J) == 0;
-    return (lower == up) ? (key < other ? key : other) : (key > other ? key : other);
-}
-
-// ascending sort of one key per lane across the wave
-__device__ __forceinline__ uint32_t wave_sort(uint32_t key, uint32_t lane) {
-    key = bitonic_stage<2, 1>(key, lane);
-    key = bitonic_stage<4, 2>(key, lane);
-    key = bitonic_stage<4, 1>(key, lane);
-    key = bitonic_stage<8, 4>(key, lane);
-    key = bitonic_stage<8, 2>(key, lane);
-    key = bitonic_stage<8, 1>(key, lane);
-    key = bitonic_stage<16, 8>(key, lane);
-    key = bitonic_stage<16, 4>(key, lane);
-    key = bitonic_stage<16, 2>(key, lane);
-    key = bitonic_stage<16, 1>(key, lane);
-    key = bitonic_stage<32, 16>(key, lane);
-    key = bitonic_stage<32, 8>(key, lane);
-    key = bitonic_stage<32, 4>(key, lane);
-    key = bitonic_stage<32, 2>(key, lane);
-    key = bitonic_stage<32, 1>(key, lane);
-    key = bitonic_stage<64, 32>(key, lane);
-    key = bitonic_stage<64, 16>(key, lane);
-    key = bitonic_stage<64, 8>(key, lane);
-    key = bitonic_stage<64, 4>(key, lane);
-    key = bitonic_stage<64, 2>(key, lane);
-    key = bitonic_stage<64, 1>(key, lane);
-    return key;
+    return ((uint64_t)hi << 32) | lo;
 }
 
 __device__ __forceinline__ int32_t ext_len(int32_t x) { return x >= 15 ? 1 + (x - 15) / 255 : 0; }
@@ -197,24 +162,23 @@ __device__ __forceinline__ int32_t emit_seqs(const uint8_t* s, uint8_t* d, int32
         const uint32_t w0 = (uint32_t)__builtin_amdgcn_ds_bpermute((rel & 63) << 2, (int)v0);
         const uint32_t w1 = (uint32_t)__builtin_amdgcn_ds_bpermute((rel & 63) << 2, (int)vprev);
         if (t < ptotal) {
-            uint32_t byte;
-            if (r == 0) {
-                const int32_t ln = L < 15 ? L : 15;
-                const int32_t mn = M ? (M - 4 < 15 ? M - 4 : 15) : 0;
-                byte = (uint32_t)((ln << 4) | mn);
-            } else if (r <= EL) {
-                byte = r < EL ? 255u : (uint32_t)((L - 15) % 255);
-            } else if (r <= EL + L) {
-                byte = rel >= 0 && rel < 64 ? (w0 & 0xFFu) : rel >= -64 && rel < 0 ? (w1 & 0xFFu) : s[q];
-            } else if (r == EL + L + 1) {
-                byte = (uint32_t)(O & 0xFF);
-            } else if (r == EL + L + 2) {
-                byte = (uint32_t)(O >> 8);
-            } else {
-                const int32_t EM = ext_len(M - 4);
-                const int32_t k = r - (EL + L + 3);
-                byte = k < EM - 1 ? 255u : (uint32_t)((M - 4 - 15) % 255);
-            }
+            // every candidate byte, then one select chain (branch-free but for
+            // literals outside the two register windows)
+            const int32_t ln = L < 15 ? L : 15;
+            const int32_t mn = M ? (M - 4 < 15 ? M - 4 : 15) : 0;
+            const uint32_t tokb = (uint32_t)((ln << 4) | mn);
+            const uint32_t lext = r < EL ? 255u : (uint32_t)(L - 15) % 255u;
+            const int32_t EM = ext_len(M - 4);
+            const uint32_t mext = r - (EL + L + 3) < EM - 1 ? 255u : (uint32_t)(M - 4 - 15) % 255u;
+            const bool win0 = (uint32_t)rel < 64u, win1 = (uint32_t)(rel + 64) < 64u;
+            uint32_t litb = (win0 ? w0 : w1) & 0xFFu;
+            if (r > EL && r <= EL + L && !win0 && !win1) litb = s[q];
+            const uint32_t byte = r == 0 ? tokb
+                                  : r <= EL ? lext
+                                  : r <= EL + L ? litb
+                                  : r == EL + L + 1 ? (uint32_t)(O & 0xFF)
+                                  : r == EL + L + 2 ? (uint32_t)((O >> 8) & 0xFF)
+                                  : mext;
             d[op + ob + r] = (uint8_t)byte;
         }
     }
@@ -262,19 +226,18 @@ __device__ __forceinline__ void chunk_issue(Chunk& C, const uint8_t* s, uint32_t
     const int32_t p = p0 + (int32_t)lane;
     const bool act = p + 4 <= N;
     const uint32_t h = act ? phash<HB>(v) : (1u << HB);
-    // nearest earlier / later lane with the same hash: bitonic sort of (hash, lane)
-    const uint32_t key = wave_sort((h << 6) | lane, lane);
-    const uint32_t kprev = (uint32_t)__builtin_amdgcn_update_dpp((int)key, (int)key, 0x138, 0xF, 0xF, false);
-    const uint32_t knext = (uint32_t)__builtin_amdgcn_update_dpp((int)key, (int)key, 0x130, 0xF, 0xF, false);
-    const bool sprev = lane > 0 && (kprev >> 6) == (key >> 6);
-    const bool snext = lane < 63 && (knext >> 6) == (key >> 6);
-    const uint32_t info = (sprev ? (0x40u | (kprev & 63)) : 0u) | (snext ? 0x80u : 0u);
-    const uint32_t mine = (uint32_t)__builtin_amdgcn_ds_permute((int)((key & 63) << 2), (int)info);
+    // lanes with the same hash (one ballot per hash bit), hence the nearest
+    // earlier one (the candidate) and whether a later one exists (then this
+    // lane does not write the table)
+    const uint64_t eq = same_hash_mask<HB>(h, act);
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    const uint64_t earlier = eq & lt;
+    const bool later = (eq >> lane) > 1u;
     uint16_t* table16 = reinterpret_cast<uint16_t*>(table32);
     const uint32_t empty = BIG ? 0xFFFFFFFFu : kEmpty;
     const uint32_t old = act ? (BIG ? table32[h] : (uint32_t)table16[h]) : empty;
-    const int32_t cand = (mine & 0x40u) ? p0 + (int32_t)(mine & 63) : (old == empty ? -1 : (int32_t)old);
-    if (act && !(mine & 0x80u)) {
+    const int32_t cand = earlier ? p0 + 63 - (int32_t)__builtin_clzll(earlier) : (old == empty ? -1 : (int32_t)old);
+    if (act && !later) {
         if (BIG) {
             table32[h] = (uint32_t)p;
         } else {
@@ -309,7 +272,7 @@ __device__ __forceinline__ uint64_t chunk_finish(const Chunk& C, int32_t p0, int
 }
 
 template <bool BIG, int HB>
-__global__ __launch_bounds__(64) void pcompress_kernel(const uint8_t* __restrict__ src,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BIG || HB > 12 ? 1 : 5))) void pcompress_kernel(const uint8_t* __restrict__ src,
                                                        const int64_t* __restrict__ src_off,
                                                        const int32_t* __restrict__ src_len, uint8_t* __restrict__ dst,
                                                        const int64_t* __restrict__ dst_off,
