@@ -31,7 +31,10 @@
 
 namespace lz4m {
 
-constexpr int64_t kCoopMin = 64;   // copies longer than this go wave-cooperative
+#ifndef LZ4M_COOP_MIN
+#define LZ4M_COOP_MIN 64
+#endif
+constexpr int64_t kCoopMin = LZ4M_COOP_MIN;   // copies longer than this go wave-cooperative
 
 enum CopyKind : int { kNone = 0, kLiteral = 1, kMatch = 2 };
 
