@@ -301,15 +301,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BIG || HB > 
         Chunk A;
         int32_t L = 0, back = 0;
         uint64_t mask = 0;
+        uint32_t wnext = 0;   // the hash word of the chunk after next, loaded a chunk ahead
         if (N >= 4) {
             chunk_issue<BIG, HB>(A, s, table, 0, load_word(s, (int32_t)lane, N), N, mlast, lane);
             mask = chunk_finish(A, 0, matchlimit, L, back, lane);
+            if (68 <= N) wnext = load_word(s, 64 + (int32_t)lane, N);
         }
+        // Per chunk: issue B's loads (and the word of the chunk after B),
+        // walk A, finish B, then encode A.  No store sits between a load and
+        // its use, so every wait is for loads only (gfx9 counts stores in
+        // vmcnt, and a wait behind a variable number of stores is vmcnt(0)).
         for (int32_t p0 = 0; p0 + 4 <= N; p0 += 64) {
             const bool has_next = p0 + 68 <= N;
             Chunk B;
-            if (has_next)
-                chunk_issue<BIG, HB>(B, s, table, p0 + 64, load_word(s, p0 + 64 + (int32_t)lane, N), N, mlast, lane);
+            uint32_t wafter = 0;
+            if (has_next) {
+                chunk_issue<BIG, HB>(B, s, table, p0 + 64, wnext, N, mlast, lane);
+                if (p0 + 132 <= N) wafter = load_word(s, p0 + 128 + (int32_t)lane, N);
+            }
             // ---- greedy parse of chunk p0.  The serial walk only picks the
             // sequence starts: the first verified lane at or after the previous
             // match's end (catch-up moves a start back but not the end).
@@ -371,6 +380,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BIG || HB > 
                 q_pb = __builtin_amdgcn_ds_permute(addr, ipsz - psz);
                 anchor = cur;
             }
+            int32_t LB = 0, backB = 0;
+            uint64_t maskB = 0;
+            if (has_next) maskB = chunk_finish(B, p0 + 64, matchlimit, LB, backB, lane);
             if (ns > 0) {
                 const int32_t w = emit_seqs(s, d, op, cap, ns, q_ls, q_lit, q_off, q_ml, q_ob, q_pb, acc, pacc, p0,
                                             A.v, vprev, lane);
@@ -382,8 +394,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BIG || HB > 
             }
             if (!has_next) break;
             vprev = A.v;
-            A = B;
-            mask = chunk_finish(A, p0 + 64, matchlimit, L, back, lane);
+            A.v = B.v;
+            A.cand = B.cand;
+            mask = maskB;
+            L = LB;
+            back = backB;
+            wnext = wafter;
         }
         if (!fail) {   // last literals (lz4.c:1266-1293)
             const int32_t lit = N - anchor;
