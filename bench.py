@@ -129,9 +129,30 @@ def cpu_baseline(host_blocks: np.ndarray, comp_host: list, seconds: float = 10.0
     assert (out == BLOCK).all(), "CPU baseline decode failed"
     assert np.array_equal(dst.reshape(n, BLOCK), host_blocks[:n]), "CPU baseline output mismatch"
     val = n * reps * BLOCK / secs / GIB
-    return {"value": round(val, 3), "unit": "GiB/s", "cores": cores, "kind": cb.kind,
-            "sample": f"LZ4_decompress_safe, {n} x 64 KiB silesia-like blocks x {reps} reps "
-                      f"({secs:.1f} s, {cores} pthreads, one contiguous slice each)"}
+    res = {"value": round(val, 3), "unit": "GiB/s", "cores": cores, "kind": cb.kind,
+           "sample": f"LZ4_decompress_safe, {n} x 64 KiB silesia-like blocks x {reps} reps "
+                     f"({secs:.1f} s, {cores} pthreads, one contiguous slice each)"}
+    # the same decode on one core (all cores and 1 core), ~3 s
+    n1 = max(1, n // 8)
+    s1, _ = cb.run("decompress", 1, 1, src, src_off[:n1], lens[:n1], dst, dst_off[:n1], dst_cap[:n1])
+    r1 = max(1, int(3.0 / max(s1, 1e-3)))
+    s1, _ = cb.run("decompress", 1, r1, src, src_off[:n1], lens[:n1], dst, dst_off[:n1], dst_cap[:n1])
+    res["single_core_value"] = round(n1 * r1 * BLOCK / s1 / GIB, 3)
+    # LZ4_compress_default (the config-3 parse the GPU's ratio is compared to), all cores, ~5 s
+    raw = np.ascontiguousarray(host_blocks[:n]).reshape(-1)
+    r_off = np.arange(n, dtype=np.int64) * BLOCK
+    r_len = np.full(n, BLOCK, dtype=np.int32)
+    cstride = 65824
+    cdst = np.empty(n * cstride, dtype=np.uint8)
+    c_off = np.arange(n, dtype=np.int64) * cstride
+    c_cap = np.full(n, cstride, dtype=np.int32)
+    sc, outc = cb.run("compress", cores, 1, raw, r_off, r_len, cdst, c_off, c_cap)
+    rc = max(1, int(5.0 / max(sc, 1e-3)))
+    sc, outc = cb.run("compress", cores, rc, raw, r_off, r_len, cdst, c_off, c_cap)
+    assert (outc > 0).all(), "CPU baseline compress failed"
+    res["compress_value"] = round(n * rc * BLOCK / sc / GIB, 3)
+    res["compress_sample"] = f"LZ4_compress_default, same {n} blocks x {rc} reps ({sc:.1f} s, {cores} pthreads)"
+    return res
 
 
 def main():
