@@ -287,7 +287,9 @@ def main():
     # streams (copy in || decode || copy out)
     if args.e2e_blocks > 0:
         import lz4.block as LB
-        ne = min(args.e2e_blocks, n)
+        # every rank pins its own host buffers (24 GiB at 256 K blocks): at
+        # N > 1 a quarter of that per rank keeps a node's pinned memory modest
+        ne = min(args.e2e_blocks if world == 1 else args.e2e_blocks // 4, n)
         e_comp_bytes = int(c_off[ne - 1]) + int(c_len[ne - 1]) if ne < n else comp_total
         h_comp = torch.empty(e_comp_bytes, dtype=torch.uint8, pin_memory=True)
         h_comp.copy_(comp[:e_comp_bytes])
