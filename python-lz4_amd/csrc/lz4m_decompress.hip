@@ -836,6 +836,246 @@ __global__ __launch_bounds__(256, 4) void stage_decompress_kernel(const uint8_t*
     }
 }
 
+// ------------------------------------------------- cooperative (small batches)
+// One wavefront per block, for batches too small to fill the lane decoder
+// (it needs ~1 M blocks for full rate: a lane decodes 64 KiB in ~34 ms) --
+// single-block calls, and frames of 4 MiB blocks (2 048 lanes).  The wave
+// decodes the block's fast-loop prefix cooperatively, then lane 0 finishes the
+// block with the exact state machine (decode_step, as the chain kernel does).
+//
+// A round takes up to 64 sequences: the wave stages 1 KiB of input in LDS,
+// every lane parses a speculative sequence at position pos + lane, and a
+// readlane walk follows the chain of starts; sequence k is then re-parsed in
+// lane k, a prefix sum places it, literals are written, and matches are copied
+// in passes (a match is ready once its source ends before the first pending
+// match's start, so everything it reads is final).  Longer literals run one
+// sequence at a time on the whole wave.  A sequence is taken only when the
+// reference provably stays in its fast loop and succeeds on it (lz4.c:2004-2110:
+// ip + 1 <= iend - 17 or the long-literal margins, a single match-length byte
+// inside iend - 4, 1 <= offset <= output so far, op + ml < oend - 64);
+// anything else -- the tail, offset 0, errors -- goes to the exact path with
+// the state the reference would have, so bytes and statuses are identical.
+constexpr int kCoopIn = 1024;
+
+__device__ __forceinline__ void coop_put(uint8_t* p, u32x4 v, int32_t k) {
+    if (k >= 16) {
+        st16(p, v);
+    } else if (k > 0) {
+        put_exact(p, v, (uint32_t)k);
+    }
+}
+
+__device__ __forceinline__ int32_t coop_incl_sum(int32_t v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);   // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);   // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);   // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);   // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);   // row_bcast:15
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);   // row_bcast:31
+    return v;
+}
+
+// Exact-length whole-wave copies (no wild bytes: other sequences' output may
+// already sit right after them).
+__device__ __forceinline__ void coop_copy_literal(uint8_t* d, const uint8_t* s, int32_t len, uint32_t lane) {
+    for (int32_t base = 0; base < len; base += 16 * kWave) {
+        const int32_t pos = base + 16 * (int32_t)lane;
+        if (pos < len) coop_put(d + pos, ld16(s + pos), len - pos);
+    }
+}
+
+__device__ __forceinline__ void coop_copy_match(uint8_t* d, int32_t off, int32_t len, uint32_t lane) {
+    if (off >= 16) {
+        const int32_t w = (off < 16 * kWave ? off : 16 * kWave) & ~15;   // rows whose sources precede them
+        for (int32_t base = 0; base < len; base += w) {
+            const int32_t pos = base + 16 * (int32_t)lane;
+            if (pos < base + w && pos < len) coop_put(d + pos, ld16(d + pos - off), len - pos);
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        }
+        return;
+    }
+    const u32x4 pat = period_pattern(ld16(d - off), (uint32_t)off);
+    const int32_t step = 16 - (16 % off);
+    for (int32_t pos = step * (int32_t)lane; pos < len; pos += step * kWave) coop_put(d + pos, pat, len - pos);
+}
+
+__global__ __launch_bounds__(256) void coop_decompress_kernel(const uint8_t* __restrict__ src,
+                                                              const int64_t* __restrict__ src_off,
+                                                              const int32_t* __restrict__ src_len, uint8_t* dst,
+                                                              const int64_t* __restrict__ dst_off,
+                                                              const int32_t* __restrict__ dst_cap,
+                                                              int32_t* __restrict__ status, int64_t n) {
+    __shared__ __attribute__((aligned(16))) uint8_t ins[4][kCoopIn + 64];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    lds_u8* IN = (lds_u8*)ins[wv];
+    // static assignment (an atomic work queue in this loop nest compiled to
+    // a kernel that hung, tools/micro/coop_decode.hip)
+    for (int64_t b = (int64_t)blockIdx.x * 4 + wv; b < n; b += (int64_t)gridDim.x * 4) {
+        const uint8_t* s = src + src_off[b];
+        uint8_t* d = dst + dst_off[b];
+        const int32_t iend = src_len[b], oend = dst_cap[b];
+        if (oend < 0 || iend <= 0 || oend == 0) {   // lz4.c:1950, :1978-1983
+            if (lane == 0) status[b] = (oend == 0 && iend == 1 && s[0] == 0) ? 0 : -1;
+            continue;
+        }
+        const bool fast = oend >= 64;
+        int32_t ip = 0, op = 0;
+        while (fast) {
+            const int32_t ib = ip & ~15;
+            {
+                const int32_t x = ib + 16 * (int32_t)lane;
+                const u32x4 v = x + 16 <= iend ? ld16(s + x) : ld16_guarded(s + x, iend - x);
+                lds_st16(IN + 16 * lane, v);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            // speculative parse + walk: lane k gets the k-th sequence start
+            int32_t myseq = 0;
+            int nseq = 0;
+            bool stop = false;
+            int32_t pos = ip - ib;
+            while (nseq < 64 && pos + 80 <= kCoopIn) {
+                const u32x4 w = lds_ld16(IN + pos + (int32_t)lane);
+                const uint32_t tok = w.x & 0xFFu, lit = tok >> 4, mlc = tok & 15u;
+                bool simple = lit <= 12;
+                int32_t adv = 3 + (int32_t)lit;
+                if (mlc == 15) {
+                    simple = simple && byte_of(w, (int)(3 + (lit < 12 ? lit : 12))) != 255u;
+                    adv += 1;
+                }
+                const int32_t nxt = (int32_t)lane + adv;
+                const uint64_t smask = __ballot(simple);
+                int32_t sidx = 0;
+                while (sidx < 64 && nseq < 64) {
+                    if (!((smask >> sidx) & 1ull)) {
+                        stop = true;
+                        break;
+                    }
+                    if ((int)lane == nseq) myseq = pos + sidx;
+                    ++nseq;
+                    sidx = __builtin_amdgcn_readlane(nxt, sidx);
+                }
+                pos += sidx;
+                if (stop) break;
+            }
+            if (nseq == 0) {
+                // one sequence with literal > 12 bytes (or a long length), whole wave
+                const uint32_t tok = s[ip];
+                int32_t lit = (int32_t)(tok >> 4), ml = (int32_t)(tok & 15u), q = ip + 1;
+                if (lit == 15) {
+                    uint32_t x = 255;
+                    while (x == 255 && q < iend - 48) {
+                        x = s[q++];
+                        lit += (int32_t)x;
+                    }
+                    if (x == 255 || q + lit > iend - 32 || op + lit > oend - 32) break;   // lz4.c:2016-2027
+                } else if (q > iend - 17) {
+                    break;   // lz4.c:2034
+                }
+                const int32_t opm = op + lit;
+                const int32_t off = (int32_t)s[q + lit] | ((int32_t)s[q + lit + 1] << 8);
+                int32_t qe = q + lit + 2;
+                if (ml == 15) {
+                    uint32_t x = 255;
+                    while (x == 255 && qe < iend - 5) {
+                        x = s[qe++];
+                        ml += (int32_t)x;
+                    }
+                    if (x == 255 || qe > iend - 5) break;
+                }
+                ml += 4;
+                if (off < 1 || off > opm || opm + ml >= oend - 64) break;
+                coop_copy_literal(d + op, s + q, lit, lane);
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+                coop_copy_match(d + opm, off, ml, lane);
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+                op = opm + ml;
+                ip = qe;
+                continue;
+            }
+            // sequence k in lane k
+            const bool act = (int)lane < nseq;
+            const u32x4 w = lds_ld16(IN + (act ? myseq : 0));
+            const uint32_t tok = w.x & 0xFFu, mlc = tok & 15u;
+            const int32_t lit = (int32_t)(tok >> 4);
+            const int32_t lw = lit < 12 ? lit : 12;
+            const int32_t off = (int32_t)(window_dword(w, (uint32_t)(1 + lw)) & 0xFFFFu);
+            int32_t ml = (int32_t)mlc + 4, adv = 3 + lit;
+            if (mlc == 15) {
+                ml = 19 + (int32_t)byte_of(w, 3 + lw);
+                adv += 1;
+            }
+            const int32_t len = act ? lit + ml : 0;
+            const int32_t o = op + coop_incl_sum(len) - len;
+            const int32_t sabs = ib + myseq;
+            const bool ok = act && sabs + 1 <= iend - 17 && (mlc != 15 || sabs + adv <= iend - 4) && off >= 1 &&
+                            off <= o + lit && o + len < oend - 64;
+            const uint64_t bad = __ballot(act) & ~__ballot(ok);
+            const int use = bad ? __builtin_ctzll(bad) : nseq;
+            if (use == 0) break;
+            const bool u = (int)lane < use;
+            if (u && lit > 0) put_exact(d + o, window_shift1(w), (uint32_t)lit);
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            const int32_t m = o + lit;
+            const int32_t src_end = m - off + (off < ml ? off : ml);
+            uint64_t pend = __ballot(u);
+            while (pend) {
+                const int32_t E = __builtin_amdgcn_readlane(m, __builtin_ctzll(pend));
+                const bool ready = ((pend >> lane) & 1ull) && src_end <= E;
+                if (ready) {
+                    if (off >= 16) {
+                        for (int32_t i = 0; i < ml; i += 16) coop_put(d + m + i, ld16(d + m - off + i), ml - i);
+                    } else {
+                        const u32x4 pat = period_pattern(ld16(d + m - off), (uint32_t)off);
+                        const int32_t step = 16 - (16 % off);
+                        for (int32_t i = 0; i < ml; i += step) coop_put(d + m + i, pat, ml - i);
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+                pend &= ~__ballot(ready);
+            }
+            op = __builtin_amdgcn_readlane(o + len, use - 1);
+            ip = ib + __builtin_amdgcn_readlane(myseq + adv, use - 1);
+            if (use < nseq) break;
+        }
+        // the rest with the exact state machine on lane 0, long copies on the wave
+        Lane L;
+        L.live = false;
+        L.result = -1;
+        if (lane == 0) {
+            L.src = s;
+            L.dst = d;
+            L.iend = iend;
+            L.oend = oend;
+            L.ip = ip;
+            L.op = op;
+            L.dict_len = 0;
+            L.dict_end = d;
+            L.fast = fast;
+            L.live = true;
+        }
+        while (__any(L.live)) {
+            Copy lc{kNone, 0, 0, 0}, mc{kNone, 0, 0, 0};
+            if (L.live) decode_step<false, false>(L, lc, mc);
+            if (__ballot(lc.kind != kNone || mc.kind != kNone) == 0) continue;
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            const int64_t oe = readlane64(L.oend, 0);
+            if (__builtin_amdgcn_readlane(lc.kind, 0) != kNone) {
+                const int64_t ie = readlane64(L.iend, 0);
+                const int64_t dp = readlane64(lc.dpos, 0), sp = readlane64(lc.arg, 0), ln = readlane64(lc.len, 0);
+                wave_literal(d + dp, s + sp, ln, oe - dp, ie - sp, lane);
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            }
+            if (__builtin_amdgcn_readlane(mc.kind, 0) != kNone) {
+                const int64_t dp = readlane64(mc.dpos, 0), mo = readlane64(mc.arg, 0), ln = readlane64(mc.len, 0);
+                wave_match(d + dp, mo, ln, oe - dp, lane);
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            }
+        }
+        const int32_t r = __builtin_amdgcn_readlane(L.result, 0);
+        if (lane == 0) status[b] = r;
+    }
+}
+
 // Linked-block frames (lz4frame.c:1853-1856, LZ4F_updateDict): block i may
 // reference the output of blocks < i, so the chain decodes in order on one
 // wavefront, contiguously into dst.  Lane 0 parses; the wave runs the long
@@ -966,6 +1206,22 @@ extern "C" int lz4m_decompress_batch_ws(const uint8_t* d_src, const int64_t* d_s
     }
     if (d_work == nullptr || work_bytes < lz4m_decompress_workspace_bytes() || ((uintptr_t)d_work & 7) != 0)
         return LZ4M_EINVAL;
+    // small batches (single calls, frames of 4 MiB blocks): one wave per block.
+    // LZ4M_DECODER=lane / =coop force either decoder; LZ4M_COOP_MAX_BLOCKS
+    // moves the switch-over (default 8192 blocks).
+    static const int coop_mode = [] {
+        const char* e = getenv("LZ4M_DECODER");
+        if (e != nullptr && strcmp(e, "lane") == 0) return 0;
+        if (e != nullptr && strcmp(e, "coop") == 0) return 2;
+        return 1;
+    }();
+    static const int coop_max = env_int("LZ4M_COOP_MAX_BLOCKS", 8192);
+    if (coop_mode == 2 || (coop_mode == 1 && n <= coop_max)) {
+        const int64_t grid = (n + 3) / 4;
+        hipLaunchKernelGGL(coop_decompress_kernel, dim3((uint32_t)(grid < 65536 ? grid : 65536)), dim3(256), 0,
+                           (hipStream_t)stream, d_src, d_src_off, d_src_len, d_dst, d_dst_off, d_dst_cap, d_status, n);
+        return (int)hipGetLastError();
+    }
     // LZ4M_SLOW_BATCH: waiting lanes that trigger a general step (tuning)
     static const int slow_batch = env_int("LZ4M_SLOW_BATCH", 6);
     hipError_t e = hipMemsetAsync(d_work, 0, sizeof(unsigned long long), (hipStream_t)stream);
