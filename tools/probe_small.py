@@ -45,5 +45,8 @@ def case(nb, bs):
           flush=True)
 
 
-for nb, bs in [(1, 65536), (64, 65536), (2048, 65536), (16384, 65536), (2048, 4 << 20)]:
+sizes = os.environ.get("SIZES")
+todo = [tuple(int(x) for x in t.split("x")) for t in sizes.split(",")] if sizes else \
+    [(1, 65536), (64, 65536), (2048, 65536), (16384, 65536), (2048, 4 << 20)]
+for nb, bs in todo:
     case(nb, bs)
