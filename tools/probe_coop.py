@@ -26,11 +26,14 @@ for kind in os.environ.get("KINDS", "silesia,text").split(","):
     N.launch_compress(src, so, sl, slots, soff, scap, olen, n, N.TABLE_U16_HASH4, 1)
     dst = torch.zeros(n * 65536, dtype=torch.uint8, device=dev)
     prog = torch.zeros(2 * n, dtype=torch.int32, device=dev)
-    q = torch.zeros(1, dtype=torch.int64, device=dev)
+    q = torch.zeros(4, dtype=torch.int64, device=dev)
     run = lambda: lib.coop_decode(slots.data_ptr(), soff.data_ptr(), olen.data_ptr(), dst.data_ptr(), so.data_ptr(),
                                   sl.data_ptr(), prog.data_ptr(), n, q.data_ptr(), grid, None)
     assert run() == 0
     torch.cuda.synchronize()
+    r, p_, sg, sq = q.tolist()
+    print(f"{kind}: per block {r / n:.1f} rounds, {p_ / max(r, 1):.2f} passes/round, {sg / n:.1f} single steps, "
+          f"{sq / max(r - sg, 1):.1f} sequences/round", flush=True)
     ts = []
     for _ in range(3):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
