@@ -899,6 +899,60 @@ __device__ __forceinline__ void coop_copy_match(uint8_t* d, int32_t off, int32_t
     for (int32_t pos = step * (int32_t)lane; pos < len; pos += step * kWave) coop_put(d + pos, pat, len - pos);
 }
 
+// The sequence starting at t (relative to the LDS input window), w = its
+// first 16 bytes.  `simple`: parallel-path material -- at most one extra
+// length byte each for literal and match (< 255), and the whole sequence
+// inside the window.  Literals of <= 12 bytes come from w, longer ones from LDS.
+struct CoopSeq {
+    int32_t lit, litpos, off, ml, adv;
+    bool simple, litx, mlx;
+};
+
+__device__ __forceinline__ CoopSeq coop_parse(const lds_u8* IN, int32_t t, u32x4 w) {
+    CoopSeq q;
+    const uint32_t tok = w.x & 0xFFu, mlc = tok & 15u;
+    int32_t lit = (int32_t)(tok >> 4);
+    q.litx = lit == 15;
+    q.mlx = mlc == 15;
+    q.simple = true;
+    if (lit <= 12) {
+        q.lit = lit;
+        q.litpos = t + 1;
+        q.off = (int32_t)(window_dword(w, (uint32_t)(1 + lit)) & 0xFFFFu);
+        q.ml = (int32_t)mlc + 4;
+        q.adv = 3 + lit;
+        if (q.mlx) {
+            const uint32_t e = byte_of(w, 3 + lit);
+            q.simple = e != 255u;
+            q.ml = 19 + (int32_t)e;
+            q.adv += 1;
+        }
+        return q;
+    }
+    int32_t lp = t + 1;
+    if (q.litx) {
+        const uint32_t b = IN[t + 1];
+        q.simple = b != 255u;
+        lit += (int32_t)b;
+        lp = t + 2;
+    }
+    q.lit = lit;
+    q.litpos = lp;
+    const int32_t po = lp + lit;   // offset position
+    q.simple = q.simple && po + 3 + 16 <= kCoopIn;
+    const int32_t pc = q.simple ? po : 0;
+    q.off = (int32_t)IN[pc] | ((int32_t)IN[pc + 1] << 8);
+    q.ml = (int32_t)mlc + 4;
+    q.adv = po + 2 - t;
+    if (q.mlx) {
+        const uint32_t e = IN[pc + 2];
+        q.simple = q.simple && e != 255u;
+        q.ml = 19 + (int32_t)e;
+        q.adv += 1;
+    }
+    return q;
+}
+
 __global__ __launch_bounds__(256) void coop_decompress_kernel(const uint8_t* __restrict__ src,
                                                               const int64_t* __restrict__ src_off,
                                                               const int32_t* __restrict__ src_len, uint8_t* dst,
@@ -934,15 +988,9 @@ __global__ __launch_bounds__(256) void coop_decompress_kernel(const uint8_t* __r
             bool stop = false;
             int32_t pos = ip - ib;
             while (nseq < 64 && pos + 80 <= kCoopIn) {
-                const u32x4 w = lds_ld16(IN + pos + (int32_t)lane);
-                const uint32_t tok = w.x & 0xFFu, lit = tok >> 4, mlc = tok & 15u;
-                bool simple = lit <= 12;
-                int32_t adv = 3 + (int32_t)lit;
-                if (mlc == 15) {
-                    simple = simple && byte_of(w, (int)(3 + (lit < 12 ? lit : 12))) != 255u;
-                    adv += 1;
-                }
-                const int32_t nxt = (int32_t)lane + adv;
+                const CoopSeq q = coop_parse(IN, pos + (int32_t)lane, lds_ld16(IN + pos + (int32_t)lane));
+                const bool simple = q.simple;
+                const int32_t nxt = (int32_t)lane + q.adv;
                 const uint64_t smask = __ballot(simple);
                 int32_t sidx = 0;
                 while (sidx < 64 && nseq < 64) {
@@ -994,26 +1042,29 @@ __global__ __launch_bounds__(256) void coop_decompress_kernel(const uint8_t* __r
             }
             // sequence k in lane k
             const bool act = (int)lane < nseq;
-            const u32x4 w = lds_ld16(IN + (act ? myseq : 0));
-            const uint32_t tok = w.x & 0xFFu, mlc = tok & 15u;
-            const int32_t lit = (int32_t)(tok >> 4);
-            const int32_t lw = lit < 12 ? lit : 12;
-            const int32_t off = (int32_t)(window_dword(w, (uint32_t)(1 + lw)) & 0xFFFFu);
-            int32_t ml = (int32_t)mlc + 4, adv = 3 + lit;
-            if (mlc == 15) {
-                ml = 19 + (int32_t)byte_of(w, 3 + lw);
-                adv += 1;
-            }
+            const int32_t tk = act ? myseq : 0;
+            const u32x4 w = lds_ld16(IN + tk);
+            const CoopSeq q = coop_parse(IN, tk, w);
+            const int32_t lit = q.lit, off = q.off, ml = q.ml, adv = q.adv;
             const int32_t len = act ? lit + ml : 0;
             const int32_t o = op + coop_incl_sum(len) - len;
             const int32_t sabs = ib + myseq;
-            const bool ok = act && sabs + 1 <= iend - 17 && (mlc != 15 || sabs + adv <= iend - 4) && off >= 1 &&
+            // the reference's fast-loop margins (lz4.c:2004-2110, as fast_seq / decode_step)
+            const bool lit_ok = q.litx ? ib + q.litpos + lit <= iend - 32 && o + lit <= oend - 32
+                                       : sabs + 1 <= iend - 17;
+            const bool ok = act && q.simple && lit_ok && (!q.mlx || sabs + adv <= iend - 4) && off >= 1 &&
                             off <= o + lit && o + len < oend - 64;
             const uint64_t bad = __ballot(act) & ~__ballot(ok);
             const int use = bad ? __builtin_ctzll(bad) : nseq;
             if (use == 0) break;
             const bool u = (int)lane < use;
-            if (u && lit > 0) put_exact(d + o, window_shift1(w), (uint32_t)lit);
+            if (u && lit > 0) {
+                if (lit <= 12) {
+                    put_exact(d + o, window_shift1(w), (uint32_t)lit);
+                } else {
+                    for (int32_t i = 0; i < lit; i += 16) coop_put(d + o + i, lds_ld16(IN + q.litpos + i), lit - i);
+                }
+            }
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
             const int32_t m = o + lit;
             const int32_t src_end = m - off + (off < ml ? off : ml);

@@ -20,7 +20,7 @@ mode = os.environ.get("LZ4M_DECODER", "auto")
 
 def case(nb, bs):
     per = bs // 65536
-    src = B.make_batch(nb * per, min(4096, nb * per), "silesia", 7, dev)
+    src = B.make_batch(nb * per, min(4096, nb * per), os.environ.get("KIND", "silesia"), 7, dev)
     so = torch.arange(nb, dtype=torch.int64, device=dev) * bs
     sl = torch.full((nb,), bs, dtype=torch.int32, device=dev)
     cap = ((bs + bs // 255 + 16 + 15) // 16) * 16
