@@ -953,6 +953,48 @@ __device__ __forceinline__ CoopSeq coop_parse(const lds_u8* IN, int32_t t, u32x4
     return q;
 }
 
+// The block's rest from (ip, op) with the exact state machine on lane 0 and
+// long copies on the whole wave (as decompress_chain_kernel); returns the
+// reference's result (decoded size or -(error position)-1).  Output [0, op)
+// must already be in HBM and visible to the wave.
+__device__ __forceinline__ int32_t coop_finish(const uint8_t* s, uint8_t* d, int32_t iend, int32_t oend, int32_t ip,
+                                               int32_t op, bool fast, uint32_t lane) {
+    Lane L;
+    L.live = false;
+    L.result = -1;
+    if (lane == 0) {
+        L.src = s;
+        L.dst = d;
+        L.iend = iend;
+        L.oend = oend;
+        L.ip = ip;
+        L.op = op;
+        L.dict_len = 0;
+        L.dict_end = d;
+        L.fast = fast;
+        L.live = true;
+    }
+    while (__any(L.live)) {
+        Copy lc{kNone, 0, 0, 0}, mc{kNone, 0, 0, 0};
+        if (L.live) decode_step<false, false>(L, lc, mc);
+        if (__ballot(lc.kind != kNone || mc.kind != kNone) == 0) continue;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        const int64_t oe = readlane64(L.oend, 0);
+        if (__builtin_amdgcn_readlane(lc.kind, 0) != kNone) {
+            const int64_t ie = readlane64(L.iend, 0);
+            const int64_t dp = readlane64(lc.dpos, 0), sp = readlane64(lc.arg, 0), ln = readlane64(lc.len, 0);
+            wave_literal(d + dp, s + sp, ln, oe - dp, ie - sp, lane);
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        }
+        if (__builtin_amdgcn_readlane(mc.kind, 0) != kNone) {
+            const int64_t dp = readlane64(mc.dpos, 0), mo = readlane64(mc.arg, 0), ln = readlane64(mc.len, 0);
+            wave_match(d + dp, mo, ln, oe - dp, lane);
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        }
+    }
+    return __builtin_amdgcn_readlane(L.result, 0);
+}
+
 __global__ __launch_bounds__(256) void coop_decompress_kernel(const uint8_t* __restrict__ src,
                                                               const int64_t* __restrict__ src_off,
                                                               const int32_t* __restrict__ src_len, uint8_t* dst,
@@ -1089,42 +1131,287 @@ __global__ __launch_bounds__(256) void coop_decompress_kernel(const uint8_t* __r
             if (use < nseq) break;
         }
         // the rest with the exact state machine on lane 0, long copies on the wave
-        Lane L;
-        L.live = false;
-        L.result = -1;
-        if (lane == 0) {
-            L.src = s;
-            L.dst = d;
-            L.iend = iend;
-            L.oend = oend;
-            L.ip = ip;
-            L.op = op;
-            L.dict_len = 0;
-            L.dict_end = d;
-            L.fast = fast;
-            L.live = true;
-        }
-        while (__any(L.live)) {
-            Copy lc{kNone, 0, 0, 0}, mc{kNone, 0, 0, 0};
-            if (L.live) decode_step<false, false>(L, lc, mc);
-            if (__ballot(lc.kind != kNone || mc.kind != kNone) == 0) continue;
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-            const int64_t oe = readlane64(L.oend, 0);
-            if (__builtin_amdgcn_readlane(lc.kind, 0) != kNone) {
-                const int64_t ie = readlane64(L.iend, 0);
-                const int64_t dp = readlane64(lc.dpos, 0), sp = readlane64(lc.arg, 0), ln = readlane64(lc.len, 0);
-                wave_literal(d + dp, s + sp, ln, oe - dp, ie - sp, lane);
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-            }
-            if (__builtin_amdgcn_readlane(mc.kind, 0) != kNone) {
-                const int64_t dp = readlane64(mc.dpos, 0), mo = readlane64(mc.arg, 0), ln = readlane64(mc.len, 0);
-                wave_match(d + dp, mo, ln, oe - dp, lane);
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-            }
-        }
-        const int32_t r = __builtin_amdgcn_readlane(L.result, 0);
+        const int32_t r = coop_finish(s, d, iend, oend, ip, op, fast, lane);
         if (lane == 0) status[b] = r;
     }
+}
+
+// ------------------------------------ cooperative with on-chip history
+// hist_decompress_kernel: the cooperative decoder above with the block's
+// output assembled in an 8 KiB LDS buffer per wave instead of in HBM.  The
+// buffer holds output [base, base + kHistW); a round's literals and matches
+// are written there with exact byte counts, the readiness passes read match
+// sources from it (an LDS round trip per pass instead of an HBM one), and
+// only sources older than `base` (more than ~4 KiB back) come from HBM.  After
+// each round the finished 16-byte chunks leave for HBM in one coalesced pass
+// ([0, F) is in HBM).  When the buffer fills, its last kHistKeep bytes move to
+// the front (rebase).  Long literals and the exact tail run on HBM as in the
+// cooperative kernel: everything is flushed first and the history reloaded
+// after.  The accept/reject rules are the cooperative kernel's plus "fits in
+// the buffer", so statuses and bytes are identical.
+constexpr int32_t kHistW = 8192;
+constexpr int32_t kHistKeep = 4096;
+constexpr int32_t kHistRebase = kHistW - 2048;
+constexpr int32_t kHistRestage = 384;
+
+// Store exactly k bytes (k >= 16: all 16) of v at LDS address p.
+__device__ __forceinline__ void lds_put_exact(lds_u8* p, u32x4 v, int32_t k) {
+    if (k >= 16) {
+        lds_st16(p, v);
+        return;
+    }
+    if (k <= 0) return;
+    uint32_t o = 0;
+    if (k & 8) {
+        const uint64_t x = ((uint64_t)v.y << 32) | v.x;
+        __builtin_memcpy((uint8_t*)p, &x, 8);
+        o = 8;
+    }
+    if (k & 4) {
+        const uint32_t x = window_dword(v, o);
+        __builtin_memcpy((uint8_t*)(p + o), &x, 4);
+        o += 4;
+    }
+    if (k & 2) {
+        const uint16_t x = (uint16_t)window_dword(v, o);
+        __builtin_memcpy((uint8_t*)(p + o), &x, 2);
+        o += 2;
+    }
+    if (k & 1) p[o] = (uint8_t)window_dword(v, o);
+}
+
+__device__ __forceinline__ void lds_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// LZ4M_HIST_PROF (diagnostic builds only, tools/prof_hist.py): per-phase
+// cycle sums of hist_decompress_kernel, read with lz4m_hist_prof.
+#ifdef LZ4M_HIST_PROF
+__device__ unsigned long long g_hist_prof[16];
+#define HP_DECL uint64_t hp[16] = {0}; uint64_t hp_t = clock64();
+#define HP_MARK(i) do { const uint64_t _t = clock64(); hp[i] += _t - hp_t; hp_t = _t; } while (0)
+#define HP_COUNT(i, x) hp[i] += (uint64_t)(x)
+#define HP_FLUSH() do { if (lane == 0) for (int _i = 0; _i < 16; ++_i) atomicAdd(&g_hist_prof[_i], (unsigned long long)hp[_i]); } while (0)
+#else
+#define HP_DECL
+#define HP_MARK(i) do {} while (0)
+#define HP_COUNT(i, x) do {} while (0)
+#define HP_FLUSH() do {} while (0)
+#endif
+
+__global__ __launch_bounds__(256, 4) void hist_decompress_kernel(const uint8_t* __restrict__ src,
+                                                                 const int64_t* __restrict__ src_off,
+                                                                 const int32_t* __restrict__ src_len, uint8_t* dst,
+                                                                 const int64_t* __restrict__ dst_off,
+                                                                 const int32_t* __restrict__ dst_cap,
+                                                                 int32_t* __restrict__ status, int64_t n) {
+    __shared__ __attribute__((aligned(16))) uint8_t ins[4][kCoopIn + 64];
+    __shared__ __attribute__((aligned(16))) uint8_t outs[4][kHistW + 32];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    lds_u8* IN = (lds_u8*)ins[wv];
+    lds_u8* OB = (lds_u8*)outs[wv];
+    HP_DECL
+    for (int64_t b = (int64_t)blockIdx.x * 4 + wv; b < n; b += (int64_t)gridDim.x * 4) {
+        const uint8_t* s = src + src_off[b];
+        uint8_t* d = dst + dst_off[b];
+        const int32_t iend = src_len[b], oend = dst_cap[b];
+        if (oend < 0 || iend <= 0 || oend == 0) {   // lz4.c:1950, :1978-1983
+            if (lane == 0) status[b] = (oend == 0 && iend == 1 && s[0] == 0) ? 0 : -1;
+            continue;
+        }
+        const bool fast = oend >= 64;
+        int32_t ip = 0, op = 0, base = 0, F = 0, ib = -kCoopIn;
+        HP_MARK(15);
+        while (fast) {
+            HP_COUNT(8, 1);
+            if (op - base > kHistRebase) {   // keep the last kHistKeep bytes
+                const int32_t nb = (op - kHistKeep) & ~15;
+                // the move distance (> 2 KiB) exceeds the 1 KiB a wave moves per pass
+                for (int32_t c = 16 * (int32_t)lane; c < op - nb; c += 16 * kWave) {
+                    const u32x4 v = lds_ld16(OB + (nb - base) + c);
+                    lds_wait();
+                    lds_st16(OB + c, v);
+                }
+                base = nb;
+            }
+            // the 1 KiB input window serves several rounds (~3.5 input bytes per
+            // sequence): restage only when fewer than kHistRestage bytes remain
+            if (ip - ib > kCoopIn - kHistRestage) {
+                ib = ip & ~15;
+                const int32_t x = ib + 16 * (int32_t)lane;
+                const u32x4 v = x + 16 <= iend ? ld16(s + x) : ld16_guarded(s + x, iend - x);
+                lds_st16(IN + 16 * lane, v);
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            }
+            HP_MARK(0);
+            // speculative parse + walk: lane k gets the k-th sequence start
+            int32_t myseq = 0;
+            int nseq = 0;
+            bool stop = false;
+            int32_t pos = ip - ib;
+            // The chain of starts by pointer jumping instead of a 64-step readlane
+            // walk: J[s][l] = the 2^s-th successor of position pos + l (>= 64: left
+            // the 64 parsed positions; kNoSeq: after a non-simple sequence), and
+            // lane nseq + k reads the k-th start from the bits of k.
+            while (nseq < 64 && pos + 80 <= kCoopIn) {
+                const CoopSeq q = coop_parse(IN, pos + (int32_t)lane, lds_ld16(IN + pos + (int32_t)lane));
+                const uint64_t smask = __ballot(q.simple);
+                constexpr int32_t kNoSeq = 1023;
+                int32_t J[6];
+                J[0] = q.simple ? (int32_t)lane + q.adv : kNoSeq;
+#pragma unroll
+                for (int t = 1; t < 6; ++t) {
+                    const int32_t x = __builtin_amdgcn_ds_bpermute((J[t - 1] & 63) << 2, J[t - 1]);
+                    J[t] = J[t - 1] < 64 ? x : J[t - 1];
+                }
+                const int32_t kk = (int32_t)lane - nseq;
+                int32_t c = kk >= 0 ? 0 : kNoSeq;
+#pragma unroll
+                for (int t = 0; t < 6; ++t) {
+                    const int32_t x = __builtin_amdgcn_ds_bpermute((c & 63) << 2, J[t]);
+                    if (((kk >> t) & 1) && c < 64) c = x;
+                }
+                const bool valid = c < 64 && ((smask >> c) & 1ull);
+                if (valid) myseq = pos + c;
+                const int nn = nseq + (int)__builtin_popcountll(__ballot(valid));
+                if (nn >= 64) {
+                    nseq = 64;
+                    break;
+                }
+                const int32_t cv = __builtin_amdgcn_readlane(c, nn);   // the first start not taken
+                nseq = nn;
+                if (cv < 64) {   // a non-simple sequence
+                    stop = true;
+                    break;
+                }
+                pos += cv;
+            }
+            HP_MARK(1);
+            if (nseq == 0) {
+                // one sequence with literal > 12 bytes (or a long length), whole wave, on HBM
+                const uint32_t tok = s[ip];
+                int32_t lit = (int32_t)(tok >> 4), ml = (int32_t)(tok & 15u), q = ip + 1;
+                if (lit == 15) {
+                    uint32_t x = 255;
+                    while (x == 255 && q < iend - 48) {
+                        x = s[q++];
+                        lit += (int32_t)x;
+                    }
+                    if (x == 255 || q + lit > iend - 32 || op + lit > oend - 32) break;   // lz4.c:2016-2027
+                } else if (q > iend - 17) {
+                    break;   // lz4.c:2034
+                }
+                const int32_t opm = op + lit;
+                const int32_t off = (int32_t)s[q + lit] | ((int32_t)s[q + lit + 1] << 8);
+                int32_t qe = q + lit + 2;
+                if (ml == 15) {
+                    uint32_t x = 255;
+                    while (x == 255 && qe < iend - 5) {
+                        x = s[qe++];
+                        ml += (int32_t)x;
+                    }
+                    if (x == 255 || qe > iend - 5) break;
+                }
+                ml += 4;
+                if (off < 1 || off > opm || opm + ml >= oend - 64) break;
+                for (int32_t c = F + 16 * (int32_t)lane; c < op; c += 16 * kWave)
+                    coop_put(d + c, lds_ld16(OB + (c - base)), op - c);
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+                coop_copy_literal(d + op, s + q, lit, lane);
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+                coop_copy_match(d + opm, off, ml, lane);
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+                op = opm + ml;
+                ip = qe;
+                // reload the history (op < oend - 64, so the 16-byte reads stay in dst)
+                base = (op > kHistKeep ? op - kHistKeep : 0) & ~15;
+                for (int32_t c = base + 16 * (int32_t)lane; c < op; c += 16 * kWave)
+                    lds_st16(OB + (c - base), ld16(d + c));
+                F = op;
+                HP_MARK(6);
+                continue;
+            }
+            // sequence k in lane k
+            const bool act = (int)lane < nseq;
+            const int32_t tk = act ? myseq : 0;
+            const u32x4 w = lds_ld16(IN + tk);
+            const CoopSeq q = coop_parse(IN, tk, w);
+            const int32_t lit = q.lit, off = q.off, ml = q.ml, adv = q.adv;
+            const int32_t len = act ? lit + ml : 0;
+            const int32_t o = op + coop_incl_sum(len) - len;
+            const int32_t sabs = ib + myseq;
+            // the reference's fast-loop margins (lz4.c:2004-2110, as fast_seq / decode_step)
+            const bool lit_ok = q.litx ? ib + q.litpos + lit <= iend - 32 && o + lit <= oend - 32
+                                       : sabs + 1 <= iend - 17;
+            const bool ok = act && q.simple && lit_ok && (!q.mlx || sabs + adv <= iend - 4) && off >= 1 &&
+                            off <= o + lit && o + len < oend - 64 && o + len <= base + kHistW;
+            const uint64_t bad = __ballot(act) & ~__ballot(ok);
+            const int use = bad ? __builtin_ctzll(bad) : nseq;
+            if (use == 0) break;
+            HP_COUNT(10, use);
+            HP_MARK(2);
+            const bool u = (int)lane < use;
+            if (u && lit > 0) {
+                if (lit <= 12) {
+                    lds_put_exact(OB + (o - base), window_shift1(w), lit);
+                } else {
+                    for (int32_t i = 0; i < lit; i += 16)
+                        lds_put_exact(OB + (o - base + i), lds_ld16(IN + q.litpos + i), lit - i);
+                }
+            }
+            lds_wait();
+            HP_MARK(3);
+            const int32_t m = o + lit;
+            const int32_t src_end = m - off + (off < ml ? off : ml);
+            // A match is ready when no pending match writes into its source: its
+            // source ends before the first pending match, or the nearest pending
+            // match below it (pending destinations are disjoint and ordered) ends
+            // before its source starts.
+            const int32_t mend = m + ml;
+            const uint64_t below = (1ull << lane) - 1ull;
+            uint64_t pend = __ballot(u);
+            while (pend) {
+                const int32_t E = __builtin_amdgcn_readlane(m, __builtin_ctzll(pend));
+                const uint64_t pb = pend & below;
+                const int32_t J = pb ? 63 - __builtin_clzll(pb) : (int32_t)lane;
+                const int32_t endJ = __builtin_amdgcn_ds_bpermute(J << 2, mend);
+                const bool ready = ((pend >> lane) & 1ull) && (src_end <= E || pb == 0 || endJ <= m - off);
+                if (ready) {
+                    const int32_t s0 = m - off;
+                    if (off >= 16) {
+                        for (int32_t i = 0; i < ml; i += 16) {
+                            const int32_t sp = s0 + i;   // < base: flushed long ago (base <= F - 4 K)
+                            const u32x4 v = sp >= base ? lds_ld16(OB + (sp - base)) : ld16(d + sp);
+                            lds_put_exact(OB + (m - base + i), v, ml - i);
+                        }
+                    } else {   // s0 > m - 16 >= base
+                        const u32x4 pat = period_pattern(lds_ld16(OB + (s0 - base)), (uint32_t)off);
+                        const int32_t step = 16 - (16 % off);
+                        for (int32_t i = 0; i < ml; i += step) lds_put_exact(OB + (m - base + i), pat, ml - i);
+                    }
+                }
+                lds_wait();
+                pend &= ~__ballot(ready);
+                HP_COUNT(9, 1);
+            }
+            HP_MARK(4);
+            op = __builtin_amdgcn_readlane(o + len, use - 1);
+            ip = ib + __builtin_amdgcn_readlane(myseq + adv, use - 1);
+            // finished 16-byte chunks to HBM
+            for (int32_t c = F + 16 * (int32_t)lane; c + 16 <= op; c += 16 * kWave)
+                st16(d + c, lds_ld16(OB + (c - base)));
+            F += (op - F) & ~15;
+            HP_MARK(5);
+            if (use < nseq) break;
+        }
+        // flush the rest exactly, then the exact state machine from (ip, op)
+        for (int32_t c = F + 16 * (int32_t)lane; c < op; c += 16 * kWave)
+            coop_put(d + c, lds_ld16(OB + (c - base)), op - c);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        const int32_t r = coop_finish(s, d, iend, oend, ip, op, fast, lane);
+        if (lane == 0) status[b] = r;
+        HP_MARK(7);
+        HP_COUNT(11, 1);
+    }
+    HP_FLUSH();
 }
 
 // Linked-block frames (lz4frame.c:1853-1856, LZ4F_updateDict): block i may
@@ -1258,20 +1545,27 @@ extern "C" int lz4m_decompress_batch_ws(const uint8_t* d_src, const int64_t* d_s
     if (d_work == nullptr || work_bytes < lz4m_decompress_workspace_bytes() || ((uintptr_t)d_work & 7) != 0)
         return LZ4M_EINVAL;
     // small batches (single calls, frames of 4 MiB blocks): one wave per block.
-    // LZ4M_DECODER=lane / =coop force either decoder; LZ4M_COOP_MAX_BLOCKS
-    // moves the switch-over (default 32 768 blocks: for 64 KiB blocks the lane
-    // decoder takes ~30 ms up to ~64 K blocks, the cooperative one ~90 GB/s).
+    // LZ4M_DECODER=lane / =hist / =coop force a decoder; LZ4M_COOP_MAX_BLOCKS
+    // moves the switch-over (default 49 152 blocks: for 64 KiB blocks the lane
+    // decoder takes ~31 ms up to ~64 K blocks, the on-chip-history one ~125 GB/s:
+    // 49 152 blocks 25.9 vs 30.9 ms, 65 536 blocks 34.0 vs 31.3 ms).
     static const int coop_mode = [] {
         const char* e = getenv("LZ4M_DECODER");
         if (e != nullptr && strcmp(e, "lane") == 0) return 0;
         if (e != nullptr && strcmp(e, "coop") == 0) return 2;
+        if (e != nullptr && strcmp(e, "hist") == 0) return 3;
         return 1;
     }();
-    static const int coop_max = env_int("LZ4M_COOP_MAX_BLOCKS", 32768);
-    if (coop_mode == 2 || (coop_mode == 1 && n <= coop_max)) {
+    static const int coop_max = env_int("LZ4M_COOP_MAX_BLOCKS", 49152);
+    if (coop_mode >= 2 || (coop_mode == 1 && n <= coop_max)) {
         const int64_t grid = (n + 3) / 4;
-        hipLaunchKernelGGL(coop_decompress_kernel, dim3((uint32_t)(grid < 65536 ? grid : 65536)), dim3(256), 0,
-                           (hipStream_t)stream, d_src, d_src_off, d_src_len, d_dst, d_dst_off, d_dst_cap, d_status, n);
+        const dim3 g((uint32_t)(grid < 65536 ? grid : 65536));
+        if (coop_mode != 2)   // the on-chip-history kernel; LZ4M_DECODER=coop: the HBM-only one (A/B)
+            hipLaunchKernelGGL(hist_decompress_kernel, g, dim3(256), 0, (hipStream_t)stream, d_src, d_src_off,
+                               d_src_len, d_dst, d_dst_off, d_dst_cap, d_status, n);
+        else
+            hipLaunchKernelGGL(coop_decompress_kernel, g, dim3(256), 0, (hipStream_t)stream, d_src, d_src_off,
+                               d_src_len, d_dst, d_dst_off, d_dst_cap, d_status, n);
         return (int)hipGetLastError();
     }
     // LZ4M_SLOW_BATCH: waiting lanes that trigger a general step (tuning)
@@ -1325,3 +1619,14 @@ extern "C" int lz4m_decompress_chain(const uint8_t* d_src, const int64_t* d_src_
                        d_src_len, d_raw_flag, d_dst, d_status, n, max_block);
     return (int)hipGetLastError();
 }
+
+#ifdef LZ4M_HIST_PROF
+extern "C" int lz4m_hist_prof(unsigned long long* out, int reset) {
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(lz4m::g_hist_prof), sizeof(unsigned long long) * 16);
+    if (e == hipSuccess && reset) {
+        unsigned long long z[16] = {0};
+        e = hipMemcpyToSymbol(HIP_SYMBOL(lz4m::g_hist_prof), z, sizeof(z));
+    }
+    return (int)e;
+}
+#endif
