@@ -1247,29 +1247,39 @@ __global__ __launch_bounds__(256, 4) void hist_decompress_kernel(const uint8_t* 
             int nseq = 0;
             bool stop = false;
             int32_t pos = ip - ib;
-            // The chain of starts by pointer jumping instead of a 64-step readlane
-            // walk: J[s][l] = the 2^s-th successor of position pos + l (>= 64: left
-            // the 64 parsed positions; kNoSeq: after a non-simple sequence), and
-            // lane nseq + k reads the k-th start from the bits of k.
-            while (nseq < 64 && pos + 80 <= kCoopIn) {
-                const CoopSeq q = coop_parse(IN, pos + (int32_t)lane, lds_ld16(IN + pos + (int32_t)lane));
-                const uint64_t smask = __ballot(q.simple);
+            // The chain of starts by pointer jumping instead of a serial readlane
+            // walk.  Each lane parses two positions (pos + lane, pos + 64 + lane);
+            // J[p] = the 2^t-th successor of position p at step t (>= 128: left the
+            // parsed positions; kNoSeq: after a non-simple sequence).  Lane nseq + k
+            // applies bit t of k with J at step t while J is doubled for step t + 1,
+            // so the chain costs six dependent gathers.
+            while (nseq < 64 && pos + 144 <= kCoopIn) {
+                const int32_t ta = pos + (int32_t)lane, tb = ta + 64;
+                const CoopSeq qa = coop_parse(IN, ta, lds_ld16(IN + ta));
+                const CoopSeq qb = coop_parse(IN, tb, lds_ld16(IN + tb));
+                const uint64_t sa = __ballot(qa.simple), sb = __ballot(qb.simple);
                 constexpr int32_t kNoSeq = 1023;
-                int32_t J[6];
-                J[0] = q.simple ? (int32_t)lane + q.adv : kNoSeq;
-#pragma unroll
-                for (int t = 1; t < 6; ++t) {
-                    const int32_t x = __builtin_amdgcn_ds_bpermute((J[t - 1] & 63) << 2, J[t - 1]);
-                    J[t] = J[t - 1] < 64 ? x : J[t - 1];
-                }
+                int32_t ja = qa.simple ? (int32_t)lane + qa.adv : kNoSeq;
+                int32_t jb = qb.simple ? (int32_t)lane + 64 + qb.adv : kNoSeq;
                 const int32_t kk = (int32_t)lane - nseq;
                 int32_t c = kk >= 0 ? 0 : kNoSeq;
 #pragma unroll
                 for (int t = 0; t < 6; ++t) {
-                    const int32_t x = __builtin_amdgcn_ds_bpermute((c & 63) << 2, J[t]);
-                    if (((kk >> t) & 1) && c < 64) c = x;
+                    const int32_t ca = __builtin_amdgcn_ds_bpermute((c & 63) << 2, ja);
+                    const int32_t cb = __builtin_amdgcn_ds_bpermute((c & 63) << 2, jb);
+                    if (t < 5) {
+                        const int32_t aa = __builtin_amdgcn_ds_bpermute((ja & 63) << 2, ja);
+                        const int32_t ab = __builtin_amdgcn_ds_bpermute((ja & 63) << 2, jb);
+                        const int32_t ba = __builtin_amdgcn_ds_bpermute((jb & 63) << 2, ja);
+                        const int32_t bb = __builtin_amdgcn_ds_bpermute((jb & 63) << 2, jb);
+                        if (((kk >> t) & 1) && c < 128) c = c < 64 ? ca : cb;
+                        ja = ja < 128 ? (ja < 64 ? aa : ab) : ja;
+                        jb = jb < 128 ? (jb < 64 ? ba : bb) : jb;
+                    } else if (((kk >> t) & 1) && c < 128) {
+                        c = c < 64 ? ca : cb;
+                    }
                 }
-                const bool valid = c < 64 && ((smask >> c) & 1ull);
+                const bool valid = c < 128 && (((c < 64 ? sa : sb) >> (c & 63)) & 1ull);
                 if (valid) myseq = pos + c;
                 const int nn = nseq + (int)__builtin_popcountll(__ballot(valid));
                 if (nn >= 64) {
@@ -1278,7 +1288,7 @@ __global__ __launch_bounds__(256, 4) void hist_decompress_kernel(const uint8_t* 
                 }
                 const int32_t cv = __builtin_amdgcn_readlane(c, nn);   // the first start not taken
                 nseq = nn;
-                if (cv < 64) {   // a non-simple sequence
+                if (cv < 128) {   // a non-simple sequence
                     stop = true;
                     break;
                 }
@@ -1349,6 +1359,12 @@ __global__ __launch_bounds__(256, 4) void hist_decompress_kernel(const uint8_t* 
             HP_COUNT(10, use);
             HP_MARK(2);
             const bool u = (int)lane < use;
+            const int32_t m = o + lit;
+            // sources older than the buffer: their first 16 bytes are requested now,
+            // so the HBM round trip overlaps the literal phase
+            const bool far = u && m - off < base;
+            u32x4 pre = u32x4{0, 0, 0, 0};
+            if (far) pre = ld16(d + (m - off));
             if (u && lit > 0) {
                 if (lit <= 12) {
                     lds_put_exact(OB + (o - base), window_shift1(w), lit);
@@ -1359,27 +1375,31 @@ __global__ __launch_bounds__(256, 4) void hist_decompress_kernel(const uint8_t* 
             }
             lds_wait();
             HP_MARK(3);
-            const int32_t m = o + lit;
             const int32_t src_end = m - off + (off < ml ? off : ml);
             // A match is ready when no pending match writes into its source: its
             // source ends before the first pending match, or the nearest pending
             // match below it (pending destinations are disjoint and ordered) ends
             // before its source starts.
             const int32_t mend = m + ml;
-            const uint64_t below = (1ull << lane) - 1ull;
             uint64_t pend = __ballot(u);
             while (pend) {
                 const int32_t E = __builtin_amdgcn_readlane(m, __builtin_ctzll(pend));
-                const uint64_t pb = pend & below;
-                const int32_t J = pb ? 63 - __builtin_clzll(pb) : (int32_t)lane;
-                const int32_t endJ = __builtin_amdgcn_ds_bpermute(J << 2, mend);
-                const bool ready = ((pend >> lane) & 1ull) && (src_end <= E || pb == 0 || endJ <= m - off);
+                const bool mine = (pend >> lane) & 1ull;
+                // end of the nearest pending match below: exclusive max-scan (DPP)
+                int32_t x = __builtin_amdgcn_update_dpp(-1, mine ? mend : -1, 0x138, 0xF, 0xF, false);   // wave_shr:1
+                x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x111, 0xF, 0xF, false));   // row_shr:1
+                x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x112, 0xF, 0xF, false));   // row_shr:2
+                x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x114, 0xF, 0xF, false));   // row_shr:4
+                x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x118, 0xF, 0xF, false));   // row_shr:8
+                x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x142, 0xA, 0xF, false));   // row_bcast:15
+                x = max(x, __builtin_amdgcn_update_dpp(-1, x, 0x143, 0xC, 0xF, false));   // row_bcast:31
+                const bool ready = mine && (src_end <= E || x <= m - off);
                 if (ready) {
                     const int32_t s0 = m - off;
                     if (off >= 16) {
                         for (int32_t i = 0; i < ml; i += 16) {
                             const int32_t sp = s0 + i;   // < base: flushed long ago (base <= F - 4 K)
-                            const u32x4 v = sp >= base ? lds_ld16(OB + (sp - base)) : ld16(d + sp);
+                            const u32x4 v = (i == 0 && far) ? pre : sp >= base ? lds_ld16(OB + (sp - base)) : ld16(d + sp);
                             lds_put_exact(OB + (m - base + i), v, ml - i);
                         }
                     } else {   // s0 > m - 16 >= base
