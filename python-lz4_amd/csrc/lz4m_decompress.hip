@@ -1566,9 +1566,10 @@ extern "C" int lz4m_decompress_batch_ws(const uint8_t* d_src, const int64_t* d_s
         return LZ4M_EINVAL;
     // small batches (single calls, frames of 4 MiB blocks): one wave per block.
     // LZ4M_DECODER=lane / =hist / =coop force a decoder; LZ4M_COOP_MAX_BLOCKS
-    // moves the switch-over (default 49 152 blocks: for 64 KiB blocks the lane
-    // decoder takes ~31 ms up to ~64 K blocks, the on-chip-history one ~125 GB/s:
-    // 49 152 blocks 25.9 vs 30.9 ms, 65 536 blocks 34.0 vs 31.3 ms).
+    // moves the switch-over (default 98 304 blocks: for 64 KiB silesia-like
+    // blocks the lane decoder takes >= ~31 ms, the on-chip-history one ~0.36 ms
+    // per 1 K blocks: 81 920 blocks 29.8 vs 34.6 ms, 98 304 35.5 vs 35.3 ms,
+    // 131 072 47.0 vs 36.4 ms; profiles/r01g/crossover.log).
     static const int coop_mode = [] {
         const char* e = getenv("LZ4M_DECODER");
         if (e != nullptr && strcmp(e, "lane") == 0) return 0;
@@ -1576,7 +1577,7 @@ extern "C" int lz4m_decompress_batch_ws(const uint8_t* d_src, const int64_t* d_s
         if (e != nullptr && strcmp(e, "hist") == 0) return 3;
         return 1;
     }();
-    static const int coop_max = env_int("LZ4M_COOP_MAX_BLOCKS", 49152);
+    static const int coop_max = env_int("LZ4M_COOP_MAX_BLOCKS", 98304);
     if (coop_mode >= 2 || (coop_mode == 1 && n <= coop_max)) {
         const int64_t grid = (n + 3) / 4;
         const dim3 g((uint32_t)(grid < 65536 ? grid : 65536));
