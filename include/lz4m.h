@@ -71,6 +71,10 @@ const char* lz4m_version_string(void);
  * beyond its decoded size are unspecified (as in the reference).  Output
  * slots must not overlap.  Replaces the call at _block.c:357-359 and the
  * per-block call in LZ4F_decompress (lz4frame.c:1844-1847).
+ * Batches of up to 98 304 blocks (env LZ4M_COOP_MAX_BLOCKS) are decoded one
+ * wavefront per block with the recent output in LDS, larger ones one lane
+ * per block; both give identical bytes and statuses (env LZ4M_DECODER=lane
+ * or =hist forces either).
  */
 int lz4m_decompress_batch(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len,
                           uint8_t* d_dst, const int64_t* d_dst_off, const int32_t* d_dst_cap,
