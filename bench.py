@@ -260,6 +260,21 @@ def main():
         raise SystemExit(f"decompress verification failed: status_ok={ok_status} bytes_ok={ok_bytes}")
 
     extra = {}
+    # ---- extra: a mid-size batch of the same blocks (65 536), which goes to the
+    # one-wave-per-block decoder with the output in LDS (hist_decompress_kernel)
+    nm = min(65536, n)
+    dst[: nm * BLOCK].zero_()
+
+    def do_mid():
+        N.launch_decompress(comp, c_off[:nm], c_len[:nm], dst, dst_off[:nm], dst_cap[:nm], status[:nm], nm)
+
+    m_wall, m_ev = time_kernel(do_mid, args.steps, 1, world)
+    if not (bool((status[:nm] == BLOCK).all()) and torch.equal(dst[: nm * BLOCK], src[: nm * BLOCK])):
+        raise SystemExit("mid-size batch decompress verification failed")
+    extra["decompress_mid_batch"] = {"blocks": nm, "gib_s": round(world * nm * BLOCK / (m_wall / args.steps) / GIB, 2),
+                                     "kernel_ms": round(m_ev * 1e3, 3),
+                                     "kernel": "hist_decompress_kernel (one wave per block, output in LDS)"}
+
     # ---- extra (N > 1): gather compressed shards at rank 0 over RCCL ----
     if world > 1 and args.gather_blocks > 0:
         from lz4._dist import gather_compressed
