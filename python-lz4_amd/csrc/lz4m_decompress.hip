@@ -1149,10 +1149,16 @@ __global__ __launch_bounds__(256) void coop_decompress_kernel(const uint8_t* __r
 // cooperative kernel: everything is flushed first and the history reloaded
 // after.  The accept/reject rules are the cooperative kernel's plus "fits in
 // the buffer", so statuses and bytes are identical.
+#ifndef LZ4M_HIST_KEEP
+#define LZ4M_HIST_KEEP 4096
+#endif
+#ifndef LZ4M_HIST_RESTAGE
+#define LZ4M_HIST_RESTAGE 384
+#endif
 constexpr int32_t kHistW = 8192;
-constexpr int32_t kHistKeep = 4096;
+constexpr int32_t kHistKeep = LZ4M_HIST_KEEP;   // history kept on a rebase (tuning macro)
 constexpr int32_t kHistRebase = kHistW - 2048;
-constexpr int32_t kHistRestage = 384;
+constexpr int32_t kHistRestage = LZ4M_HIST_RESTAGE;   // restage below this many window bytes (tuning macro)
 
 // Store exactly k bytes (k >= 16: all 16) of v at LDS address p.
 __device__ __forceinline__ void lds_put_exact(lds_u8* p, u32x4 v, int32_t k) {
