@@ -205,7 +205,7 @@ def main():
         par_total = int(out_len.to(torch.int64).sum())
         # validity at full size: our decoder (bit-exact to LZ4_decompress_safe)
         # must restore every block
-        N.launch_decompress(slots, slot_off, out_len, dst, dst_off, dst_cap, status, n)
+        N.launch_decompress(slots, slot_off, out_len, dst, dst_off, dst_cap, status, n, src_bytes=par_total)
         assert bool((status == BLOCK).all()) and torch.equal(dst, src), "parallel-parse blocks do not round-trip"
         c3 = {"compress_gib_s": round(world * n * BLOCK / (c_wall / max(1, args.steps // 2)) / GIB, 2),
               "compress_kernel_ms": round(c_ev * 1e3, 3),

@@ -6,9 +6,10 @@
  * call into lz4libs/lz4.c and lz4libs/xxhash.c once per block; these entry
  * points replace those calls with stream-ordered, batched HIP launches over
  * device-resident blocks.  Plain pointers and sizes only: every pointer named
- * d_* is a device (HBM) pointer, `stream` is a hipStream_t.  No entry point
- * allocates, synchronises or touches host memory, so every call can be
- * captured into a hipGraph.
+ * d_* is a device (HBM) pointer, `stream` is a hipStream_t.  No batched entry
+ * point synchronises or touches host memory; only lz4m_decompress_batch
+ * allocates (64 bytes, stream-ordered), so every call can be captured into a
+ * hipGraph.
  *
  * Return value of every launcher: 0 on success, otherwise a hipError_t value
  * (launch failure) or LZ4M_EINVAL (bad argument).
@@ -71,28 +72,56 @@ const char* lz4m_version_string(void);
  * beyond its decoded size are unspecified (as in the reference).  Output
  * slots must not overlap.  Replaces the call at _block.c:357-359 and the
  * per-block call in LZ4F_decompress (lz4frame.c:1844-1847).
- * Batches of up to 98 304 blocks (env LZ4M_COOP_MAX_BLOCKS) are decoded one
- * wavefront per block with the recent output in LDS, larger ones one lane
- * per block; both give identical bytes and statuses (env LZ4M_DECODER=lane
- * or =hist forces either).
+ * Every decoder gives identical bytes and statuses; they differ in speed:
+ *   rows   -- large batches: a lane-per-block parse, then one 16-lane row per
+ *             block with its recent output in LDS, then an exact lane-per-block
+ *             finisher for each block's tail (needs the scratch of
+ *             lz4m_decompress_workspace_size);
+ *   hist   -- one wavefront per block with its recent output in LDS (small and
+ *             mid-size batches, large blocks);
+ *   lane   -- one lane per block, LDS-staged (large batches, 64 bytes of scratch);
+ *   coop, direct -- earlier designs, kept for A/B measurements.
+ * This entry point takes 64 bytes of stream-ordered scratch per call
+ * (hipMallocAsync / hipFreeAsync on `stream`), so it never uses the rows
+ * decoder; pass scratch through lz4m_decompress_batch_ws for that.
  */
 int lz4m_decompress_batch(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len,
                           uint8_t* d_dst, const int64_t* d_dst_off, const int32_t* d_dst_cap,
                           int32_t* d_status, int64_t n, lz4m_stream_t stream);
 
-/* Device scratch lz4m_decompress_batch_ws needs (the block work-queue
- * counter of the persistent decoder). */
+/* Minimum device scratch of lz4m_decompress_batch_ws (the work-queue counter
+ * of the lane decoder). */
 size_t lz4m_decompress_workspace_bytes(void);
 
-/* lz4m_decompress_batch with caller-provided device scratch of at least
- * lz4m_decompress_workspace_bytes() bytes, 8-byte aligned, not shared with a
- * concurrently running call.  lz4m_decompress_batch itself draws its scratch
- * from a small library-owned pool (1024 slots used round-robin), so use this
- * form when very many decodes may be in flight at once. */
+/* Device scratch for the fastest decode of n blocks whose compressed sizes
+ * sum to at most src_bytes: 64 + 32 n bytes of counters and per-block
+ * records, plus one byte per three compressed bytes for sequence lengths.
+ * Less scratch is accepted: blocks whose lengths do not fit are decoded by
+ * the exact finisher alone, and below 64 + 32 n + 64 bytes the rows decoder
+ * is not used. */
+size_t lz4m_decompress_workspace_size(int64_t n, int64_t src_bytes);
+
+/* lz4m_decompress_batch with caller-provided device scratch (8-byte aligned,
+ * at least lz4m_decompress_workspace_bytes(), not shared with a concurrently
+ * running call).  Picks the decoder by batch size and scratch (env
+ * LZ4M_DECODER=rows|hist|lane|coop|direct forces one; LZ4M_ROWS_MIN_BLOCKS and
+ * LZ4M_COOP_MAX_BLOCKS move the switch-overs). */
 int lz4m_decompress_batch_ws(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len,
                              uint8_t* d_dst, const int64_t* d_dst_off, const int32_t* d_dst_cap,
                              int32_t* d_status, int64_t n, void* d_work, size_t work_bytes,
                              lz4m_stream_t stream);
+
+/* lz4m_decompress_batch_ws with an explicit decoder (tests, A/B runs). */
+#define LZ4M_DECODER_AUTO   0
+#define LZ4M_DECODER_LANE   1
+#define LZ4M_DECODER_COOP   2
+#define LZ4M_DECODER_HIST   3
+#define LZ4M_DECODER_ROWS   4
+#define LZ4M_DECODER_DIRECT 5
+int lz4m_decompress_batch_sel(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len,
+                              uint8_t* d_dst, const int64_t* d_dst_off, const int32_t* d_dst_cap,
+                              int32_t* d_status, int64_t n, void* d_work, size_t work_bytes, int decoder,
+                              lz4m_stream_t stream);
 
 /*
  * Batched LZ4_decompress_safe_usingDict with the dictionary in a separate

@@ -21,6 +21,7 @@
 // window is <= 64 KiB behind).  Algorithmic HBM bytes per block =
 // compressed size + decoded size.
 #include "lz4m_common.h"
+#include "lz4m_rows.h"
 #include "../../include/lz4m.h"
 
 #include <stdlib.h>
@@ -572,7 +573,10 @@ fail:
 #undef OOW
 }
 
-template <bool DICT>
+// RESUME (the finisher of the large-batch decoder, lz4m_rows.hip): every
+// block starts at the reference's state after its good prefix, resume[i].ip /
+// .op, which rows_exec_kernel has already written to dst.
+template <bool DICT, bool RESUME = false>
 __global__ __launch_bounds__(256) void decompress_kernel(const uint8_t* __restrict__ src,
                                                          const int64_t* __restrict__ src_off,
                                                          const int32_t* __restrict__ src_len, uint8_t* dst,
@@ -581,7 +585,8 @@ __global__ __launch_bounds__(256) void decompress_kernel(const uint8_t* __restri
                                                          const uint8_t* __restrict__ dict,
                                                          const int64_t* __restrict__ dict_off,
                                                          const int32_t* __restrict__ dict_len,
-                                                         int32_t* __restrict__ status, int64_t n) {
+                                                         int32_t* __restrict__ status, int64_t n,
+                                                         const RowMeta* __restrict__ resume = nullptr) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t lane = lane_id();
     Lane L;
@@ -609,6 +614,10 @@ __global__ __launch_bounds__(256) void decompress_kernel(const uint8_t* __restri
         } else {
             L.fast = L.oend >= 64;
             L.live = true;
+            if (RESUME) {
+                L.ip = resume[i].ip;
+                L.op = resume[i].op;
+            }
         }
     }
 
@@ -1525,18 +1534,26 @@ using namespace lz4m;
 
 namespace {
 
+int current_device() {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    return dev >= 0 && dev < 64 ? dev : 0;
+}
+
 // Persistent grid for the staged decoder: every resident workgroup slot of
-// the device, no more (blocks come from the work queue).
+// the device, no more (blocks come from the work queue).  Cached per device.
 int64_t stage_grid(int64_t n) {
-    static const int64_t slots = [] {
-        int dev = 0, cus = 0, per_cu = 0;
-        (void)hipGetDevice(&dev);
+    static std::atomic<int64_t> cache[64];
+    const int dev = current_device();
+    int64_t slots = cache[dev].load(std::memory_order_relaxed);
+    if (slots == 0) {
+        int cus = 0, per_cu = 0;
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(lz4m::stage_decompress_kernel),
                                                            256, 0);
-        const int64_t s = (int64_t)(cus > 0 ? cus : 256) * (per_cu > 0 ? per_cu : 1);
-        return s;
-    }();
+        slots = (int64_t)(cus > 0 ? cus : 256) * (per_cu > 0 ? per_cu : 1);
+        cache[dev].store(slots, std::memory_order_relaxed);
+    }
     const int64_t need = (n + 255) / 256;
     return need < slots ? need : slots;
 }
@@ -1547,62 +1564,102 @@ int env_int(const char* name, int dflt) {
     return v > 0 ? v : dflt;
 }
 
+enum Decoder { kAuto = 0, kLaneDec, kCoopDec, kHistDec, kRowsDec, kDirectDec };
+
+// LZ4M_DECODER forces a decoder (A/B measurements, tests): lane | hist | coop |
+// rows | direct; unset = by batch size and scratch.
+int decoder_env() {
+    static const int mode = [] {
+        const char* e = getenv("LZ4M_DECODER");
+        if (e == nullptr) return (int)kAuto;
+        if (strcmp(e, "lane") == 0) return (int)kLaneDec;
+        if (strcmp(e, "coop") == 0) return (int)kCoopDec;
+        if (strcmp(e, "hist") == 0) return (int)kHistDec;
+        if (strcmp(e, "rows") == 0) return (int)kRowsDec;
+        if (strcmp(e, "direct") == 0) return (int)kDirectDec;
+        return (int)kAuto;
+    }();
+    return mode;
+}
+
 }  // namespace
 
 extern "C" size_t lz4m_decompress_workspace_bytes(void) { return 64; }
+
+extern "C" size_t lz4m_decompress_workspace_size(int64_t n, int64_t src_bytes) {
+    if (n <= 0) return 64;
+    const size_t lens = (size_t)(src_bytes > 0 ? src_bytes : 0) / 3 + 2 * (size_t)n + 64;
+    return (lz4m_rows_fixed_bytes(n) + lens + 255) & ~(size_t)255;
+}
+
+extern "C" int lz4m_decompress_batch_sel(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len,
+                                         uint8_t* d_dst, const int64_t* d_dst_off, const int32_t* d_dst_cap,
+                                         int32_t* d_status, int64_t n, void* d_work, size_t work_bytes, int decoder,
+                                         lz4m_stream_t stream) {
+    if (n < 0 || decoder < 0 || decoder > kDirectDec) return LZ4M_EINVAL;
+    if (n == 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    if (decoder == kAuto) decoder = decoder_env();
+    if (decoder == kDirectDec) {
+        const int64_t grid = (n + 255) / 256;
+        hipLaunchKernelGGL(decompress_kernel<false>, dim3((uint32_t)grid), dim3(256), 0, st, d_src, d_src_off,
+                           d_src_len, d_dst, d_dst_off, d_dst_cap, nullptr, nullptr, nullptr, d_status, n, nullptr);
+        return (int)hipGetLastError();
+    }
+    if (d_work == nullptr || work_bytes < lz4m_decompress_workspace_bytes() || ((uintptr_t)d_work & 7) != 0)
+        return LZ4M_EINVAL;
+    // the large-batch decoder needs scratch for its per-block records and
+    // sequence lengths (lz4m_decompress_workspace_size)
+    const bool rows_fit = work_bytes >= lz4m_rows_fixed_bytes(n) + 64;
+    // LZ4M_ROWS_MIN_BLOCKS: smallest batch sent to the row decoder (tuning)
+    static const int rows_min = env_int("LZ4M_ROWS_MIN_BLOCKS", 98305);
+    // LZ4M_COOP_MAX_BLOCKS: largest batch sent to the one-wave-per-block decoder
+    static const int coop_max = env_int("LZ4M_COOP_MAX_BLOCKS", 98304);
+    if (decoder == kAuto) {
+        if (rows_fit && n >= rows_min) decoder = kRowsDec;
+        else if (n <= coop_max) decoder = kHistDec;
+        else decoder = kLaneDec;
+    }
+    if (decoder == kRowsDec && !rows_fit) decoder = n <= coop_max ? kHistDec : kLaneDec;
+    if (decoder == kRowsDec) {
+        int pg = 1, eg = 1;
+        lz4m_rows_grids(n, &pg, &eg);
+        const int rc = lz4m_rows_launch(d_src, d_src_off, d_src_len, d_dst, d_dst_off, d_dst_cap, n, d_work, work_bytes,
+                                        pg, eg, st);
+        if (rc != 0) return rc;
+        const RowMeta* meta = reinterpret_cast<const RowMeta*>(static_cast<const uint8_t*>(d_work) + 64);
+        const int64_t grid = (n + 255) / 256;
+        hipLaunchKernelGGL((decompress_kernel<false, true>), dim3((uint32_t)grid), dim3(256), 0, st, d_src, d_src_off,
+                           d_src_len, d_dst, d_dst_off, d_dst_cap, nullptr, nullptr, nullptr, d_status, n, meta);
+        return (int)hipGetLastError();
+    }
+    if (decoder == kHistDec || decoder == kCoopDec) {
+        const int64_t grid = (n + 3) / 4;
+        const dim3 g((uint32_t)(grid < 65536 ? grid : 65536));
+        if (decoder == kHistDec)   // the on-chip-history kernel; kCoopDec: the HBM-only one (A/B)
+            hipLaunchKernelGGL(hist_decompress_kernel, g, dim3(256), 0, st, d_src, d_src_off, d_src_len, d_dst,
+                               d_dst_off, d_dst_cap, d_status, n);
+        else
+            hipLaunchKernelGGL(coop_decompress_kernel, g, dim3(256), 0, st, d_src, d_src_off, d_src_len, d_dst,
+                               d_dst_off, d_dst_cap, d_status, n);
+        return (int)hipGetLastError();
+    }
+    // LZ4M_SLOW_BATCH: waiting lanes that trigger a general step (tuning)
+    static const int slow_batch = env_int("LZ4M_SLOW_BATCH", 6);
+    hipError_t e = hipMemsetAsync(d_work, 0, sizeof(unsigned long long), st);
+    if (e != hipSuccess) return (int)e;
+    hipLaunchKernelGGL(stage_decompress_kernel, dim3((uint32_t)stage_grid(n)), dim3(256), 0, st, d_src, d_src_off,
+                       d_src_len, d_dst, d_dst_off, d_dst_cap, d_status, n, static_cast<unsigned long long*>(d_work),
+                       slow_batch);
+    return (int)hipGetLastError();
+}
 
 extern "C" int lz4m_decompress_batch_ws(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len,
                                         uint8_t* d_dst, const int64_t* d_dst_off, const int32_t* d_dst_cap,
                                         int32_t* d_status, int64_t n, void* d_work, size_t work_bytes,
                                         lz4m_stream_t stream) {
-    if (n < 0) return LZ4M_EINVAL;
-    if (n == 0) return 0;
-    // LZ4M_DECODER=direct selects the unstaged kernel (A/B measurements only)
-    static const bool direct = [] {
-        const char* e = getenv("LZ4M_DECODER");
-        return e != nullptr && strcmp(e, "direct") == 0;
-    }();
-    if (direct) {
-        const int64_t grid = (n + 255) / 256;
-        hipLaunchKernelGGL(decompress_kernel<false>, dim3((uint32_t)grid), dim3(256), 0, (hipStream_t)stream, d_src,
-                           d_src_off, d_src_len, d_dst, d_dst_off, d_dst_cap, nullptr, nullptr, nullptr, d_status, n);
-        return (int)hipGetLastError();
-    }
-    if (d_work == nullptr || work_bytes < lz4m_decompress_workspace_bytes() || ((uintptr_t)d_work & 7) != 0)
-        return LZ4M_EINVAL;
-    // small batches (single calls, frames of 4 MiB blocks): one wave per block.
-    // LZ4M_DECODER=lane / =hist / =coop force a decoder; LZ4M_COOP_MAX_BLOCKS
-    // moves the switch-over (default 98 304 blocks: for 64 KiB silesia-like
-    // blocks the lane decoder takes >= ~31 ms, the on-chip-history one ~0.36 ms
-    // per 1 K blocks: 81 920 blocks 29.8 vs 34.6 ms, 98 304 35.5 vs 35.3 ms,
-    // 131 072 47.0 vs 36.4 ms; profiles/r01g/crossover.log).
-    static const int coop_mode = [] {
-        const char* e = getenv("LZ4M_DECODER");
-        if (e != nullptr && strcmp(e, "lane") == 0) return 0;
-        if (e != nullptr && strcmp(e, "coop") == 0) return 2;
-        if (e != nullptr && strcmp(e, "hist") == 0) return 3;
-        return 1;
-    }();
-    static const int coop_max = env_int("LZ4M_COOP_MAX_BLOCKS", 98304);
-    if (coop_mode >= 2 || (coop_mode == 1 && n <= coop_max)) {
-        const int64_t grid = (n + 3) / 4;
-        const dim3 g((uint32_t)(grid < 65536 ? grid : 65536));
-        if (coop_mode != 2)   // the on-chip-history kernel; LZ4M_DECODER=coop: the HBM-only one (A/B)
-            hipLaunchKernelGGL(hist_decompress_kernel, g, dim3(256), 0, (hipStream_t)stream, d_src, d_src_off,
-                               d_src_len, d_dst, d_dst_off, d_dst_cap, d_status, n);
-        else
-            hipLaunchKernelGGL(coop_decompress_kernel, g, dim3(256), 0, (hipStream_t)stream, d_src, d_src_off,
-                               d_src_len, d_dst, d_dst_off, d_dst_cap, d_status, n);
-        return (int)hipGetLastError();
-    }
-    // LZ4M_SLOW_BATCH: waiting lanes that trigger a general step (tuning)
-    static const int slow_batch = env_int("LZ4M_SLOW_BATCH", 6);
-    hipError_t e = hipMemsetAsync(d_work, 0, sizeof(unsigned long long), (hipStream_t)stream);
-    if (e != hipSuccess) return (int)e;
-    hipLaunchKernelGGL(stage_decompress_kernel, dim3((uint32_t)stage_grid(n)), dim3(256), 0, (hipStream_t)stream,
-                       d_src, d_src_off, d_src_len, d_dst, d_dst_off, d_dst_cap, d_status, n,
-                       static_cast<unsigned long long*>(d_work), slow_batch);
-    return (int)hipGetLastError();
+    return lz4m_decompress_batch_sel(d_src, d_src_off, d_src_len, d_dst, d_dst_off, d_dst_cap, d_status, n, d_work,
+                                     work_bytes, kAuto, stream);
 }
 
 extern "C" int lz4m_decompress_batch(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len,
@@ -1610,17 +1667,15 @@ extern "C" int lz4m_decompress_batch(const uint8_t* d_src, const int64_t* d_src_
                                      int32_t* d_status, int64_t n, lz4m_stream_t stream) {
     if (n < 0) return LZ4M_EINVAL;
     if (n == 0) return 0;
-    // library-owned queue counters, used round-robin (one per call in flight)
-    constexpr int kSlots = 1024;
-    static unsigned long long* pool = nullptr;
-    static std::atomic<uint32_t> turn{0};
-    static std::once_flag once;
-    static hipError_t pool_err = hipSuccess;
-    std::call_once(once, [] { pool_err = hipMalloc(reinterpret_cast<void**>(&pool), 64 * kSlots); });
-    if (pool_err != hipSuccess) return (int)pool_err;
-    unsigned long long* slot = pool + 8 * (turn.fetch_add(1) % kSlots);
-    return lz4m_decompress_batch_ws(d_src, d_src_off, d_src_len, d_dst, d_dst_off, d_dst_cap, d_status, n, slot, 64,
-                                    stream);
+    // stream-ordered scratch for this call only (the work-queue counter of
+    // the lane decoder): no state is shared between calls in flight
+    void* work = nullptr;
+    hipError_t e = hipMallocAsync(&work, 64, (hipStream_t)stream);
+    if (e != hipSuccess) return (int)e;
+    const int rc = lz4m_decompress_batch_sel(d_src, d_src_off, d_src_len, d_dst, d_dst_off, d_dst_cap, d_status, n,
+                                             work, 64, kAuto, stream);
+    e = hipFreeAsync(work, (hipStream_t)stream);
+    return rc != 0 ? rc : (int)e;
 }
 
 extern "C" int lz4m_decompress_batch_dict(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len,
@@ -1633,7 +1688,7 @@ extern "C" int lz4m_decompress_batch_dict(const uint8_t* d_src, const int64_t* d
     const int64_t grid = (n + 255) / 256;
     hipLaunchKernelGGL(decompress_kernel<true>, dim3((uint32_t)grid), dim3(256), 0, (hipStream_t)stream, d_src,
                        d_src_off, d_src_len, d_dst, d_dst_off, d_dst_cap, d_dict, d_dict_off, d_dict_len, d_status,
-                       n);
+                       n, nullptr);
     return (int)hipGetLastError();
 }
 

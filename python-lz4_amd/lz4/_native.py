@@ -27,6 +27,8 @@ PARSE_PARALLEL = 3   # parallel-parse compressor: valid blocks, ratio of LZ4_com
 PARSE_PARALLEL_LARGE = 4   # the same for blocks > 64 KiB
 PARSE_PARALLEL_HQ = 5   # PARSE_PARALLEL with the reference's 13-bit table (ratio of LZ4_compress_default)
 EINVAL = 0x10000
+# decoder selector of lz4m_decompress_batch_sel (include/lz4m.h)
+DECODERS = {"auto": 0, "lane": 1, "coop": 2, "hist": 3, "rows": 4, "direct": 5}
 
 _lock = threading.Lock()
 _lib = None
@@ -41,6 +43,8 @@ def _declare(lib) -> None:
         "lz4m_decompress_batch": ([vp, vp, vp, vp, vp, vp, vp, i64, vp], i32),
         "lz4m_decompress_workspace_bytes": ([], C.c_size_t),
         "lz4m_decompress_batch_ws": ([vp, vp, vp, vp, vp, vp, vp, i64, vp, C.c_size_t, vp], i32),
+        "lz4m_decompress_workspace_size": ([i64, i64], C.c_size_t),
+        "lz4m_decompress_batch_sel": ([vp, vp, vp, vp, vp, vp, vp, i64, vp, C.c_size_t, i32, vp], i32),
         "lz4m_decompress_batch_dict": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, vp], i32),
         "lz4m_decompress_chain": ([vp, vp, vp, vp, vp, vp, i64, i32, vp], i32),
         "lz4m_compress_batch": ([vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, vp], i32),
@@ -106,13 +110,18 @@ def compress_bound(n: int) -> int:
 
 # ------------------------------------------------------------ raw launchers
 def launch_decompress(src, src_off, src_len, dst, dst_off, dst_cap, status, n, stream=None,
-                      dict_buf=None, dict_off=None, dict_len=None) -> None:
+                      dict_buf=None, dict_off=None, dict_len=None, decoder: str = "auto",
+                      src_bytes: int | None = None) -> None:
+    """Batched LZ4_decompress_safe(_usingDict).  ``decoder`` forces one of the
+    decoders (``DECODERS``; "auto" picks by batch size); ``src_bytes`` bounds
+    the blocks' total compressed size (default: all of ``src``) and sizes the
+    large-batch decoder's scratch."""
     L = lib()
     sp = stream_ptr(stream)
     if dict_buf is None:
-        work = _workspace(src.device, sp)
-        rc = L.lz4m_decompress_batch_ws(ptr(src), ptr(src_off), ptr(src_len), ptr(dst), ptr(dst_off), ptr(dst_cap),
-                                        ptr(status), n, ptr(work), work.numel(), sp)
+        work = _workspace(src.device, sp, n, src.numel() if src_bytes is None else src_bytes)
+        rc = L.lz4m_decompress_batch_sel(ptr(src), ptr(src_off), ptr(src_len), ptr(dst), ptr(dst_off), ptr(dst_cap),
+                                         ptr(status), n, ptr(work), work.numel(), DECODERS[decoder], sp)
     else:
         rc = L.lz4m_decompress_batch_dict(ptr(src), ptr(src_off), ptr(src_len), ptr(dst), ptr(dst_off),
                                           ptr(dst_cap), ptr(dict_buf), ptr(dict_off), ptr(dict_len), ptr(status),
@@ -123,15 +132,24 @@ def launch_decompress(src, src_off, src_len, dst, dst_off, dst_cap, status, n, s
 _WORK = {}
 
 
-def _workspace(dev, sp) -> torch.Tensor:
-    """Decoder scratch (work-queue counter), one per (device, stream): calls
-    on one stream are ordered, so they can share it."""
+def _workspace(dev, sp, n: int = 0, src_bytes: int = 0) -> torch.Tensor:
+    """Decoder scratch (lz4m_decompress_workspace_size), one buffer per
+    (device, stream), grown on demand: calls on one stream are ordered, so
+    they can share it."""
     key = (dev, sp)
+    need = int(lib().lz4m_decompress_workspace_size(n, src_bytes))
     w = _WORK.get(key)
-    if w is None:
-        w = torch.empty(int(lib().lz4m_decompress_workspace_bytes()), dtype=torch.uint8, device=dev)
+    if w is None or w.numel() < need:
+        _WORK.pop(key, None)
+        w = torch.empty(need, dtype=torch.uint8, device=dev)
         _WORK[key] = w
     return w
+
+
+def release_workspaces() -> None:
+    """Drop the cached decoder scratch (it grows to ~1/3 of the largest
+    compressed batch decoded)."""
+    _WORK.clear()
 
 
 def launch_decompress_chain(src, src_off, src_len, raw_mask, dst, status, n, max_block, stream=None) -> None:

@@ -25,7 +25,12 @@ def _pack(blocks):
     return b"".join(blocks), offs, lens
 
 
-def gpu_decompress(blocks, caps, dev):
+# every decoder (include/lz4m.h lz4m_decompress_batch_sel) must give the
+# reference's bytes and statuses; "auto" is the size-based default
+DECODERS = ["auto", "rows", "lane", "hist"]
+
+
+def gpu_decompress(blocks, caps, dev, decoder="auto"):
     packed, offs, lens = _pack(blocks)
     d_src = N.to_device(packed, dev)
     d_off, acc = [], 0
@@ -37,7 +42,7 @@ def gpu_decompress(blocks, caps, dev):
     N.launch_decompress(d_src, torch.tensor(offs, dtype=torch.int64, device=dev),
                         torch.tensor(lens, dtype=torch.int32, device=dev), d_dst,
                         torch.tensor(d_off, dtype=torch.int64, device=dev),
-                        torch.tensor(caps, dtype=torch.int32, device=dev), st, len(blocks))
+                        torch.tensor(caps, dtype=torch.int32, device=dev), st, len(blocks), decoder=decoder)
     host = d_dst.cpu().numpy()
     out = []
     for i, s in enumerate(st.cpu().tolist()):
@@ -77,11 +82,12 @@ def corpus():
     return blocks, ragged
 
 
-def test_decompress_matches_oracle(gpu, oracle, corpus):
+@pytest.mark.parametrize("decoder", DECODERS + ["coop", "direct"])
+def test_decompress_matches_oracle(gpu, oracle, corpus, decoder):
     blocks, ragged = corpus
     src = blocks + ragged + [bytes(65536), bytes([7]) * 65536, b"ab" * 32768]
     comp = [oracle.compress(b) for b in src]
-    res = gpu_decompress(comp, [len(b) for b in src], gpu)
+    res = gpu_decompress(comp, [len(b) for b in src], gpu, decoder)
     for i, (s, out) in enumerate(res):
         assert s == len(src[i]), (i, s, len(src[i]))
         assert out == src[i], i
@@ -122,11 +128,11 @@ def test_compress_large_block_u32(gpu, oracle, corpus):
     assert got == oracle.compress(big, N.TABLE_U32_HASH5)
 
 
-def test_decompress_malformed_matches_oracle(gpu, oracle, corpus):
-    blocks, _ = corpus
-    rng = random.Random(1234)
+def malformed_cases(oracle, blocks, count=3000, seed=1234):
+    """Mutated and truncated blocks with capacities around the true size."""
+    rng = random.Random(seed)
     cases, caps = [], []
-    for _ in range(3000):
+    for _ in range(count):
         b = blocks[rng.randrange(len(blocks))]
         n = rng.choice([20, 64, 100, 300, 2000, 65536])
         off = rng.randrange(0, 65536 - n + 1)
@@ -137,7 +143,14 @@ def test_decompress_malformed_matches_oracle(gpu, oracle, corpus):
             c = c[:rng.randrange(len(c) + 1)]
         cases.append(bytes(c))
         caps.append(rng.choice([n, n, n - 1, n + 1, n + 100, max(0, n - 20), 70, 0]))
-    res = gpu_decompress(cases, caps, gpu)
+    return cases, caps
+
+
+@pytest.mark.parametrize("decoder", DECODERS + ["coop", "direct"])
+def test_decompress_malformed_matches_oracle(gpu, oracle, corpus, decoder):
+    blocks, _ = corpus
+    cases, caps = malformed_cases(oracle, blocks)
+    res = gpu_decompress(cases, caps, gpu, decoder)
     for i, (s, out) in enumerate(res):
         want = oracle.decompress(cases[i], caps[i])
         assert s == want[0], (i, s, want[0], caps[i])
@@ -145,11 +158,12 @@ def test_decompress_malformed_matches_oracle(gpu, oracle, corpus):
             assert out == want[1], i
 
 
-def test_decompress_random_garbage(gpu, oracle):
+@pytest.mark.parametrize("decoder", DECODERS)
+def test_decompress_random_garbage(gpu, oracle, decoder):
     rng = np.random.default_rng(3)
     cases = [rng.integers(0, 256, size=int(rng.integers(1, 300)), dtype=np.uint8).tobytes() for _ in range(2000)]
     caps = [int(rng.integers(0, 5000)) for _ in cases]
-    res = gpu_decompress(cases, caps, gpu)
+    res = gpu_decompress(cases, caps, gpu, decoder)
     for i, (s, out) in enumerate(res):
         want = oracle.decompress(cases[i], caps[i])
         assert s == want[0], (i, s, want[0])
@@ -276,9 +290,10 @@ def test_parallel_parse_decoded_by_gpu(gpu, corpus):
         assert s == len(src[i]) and out == src[i], i
 
 
+@pytest.mark.parametrize("decoder", DECODERS)
 @pytest.mark.parametrize("kind", ["text", "source", "markup", "records", "runs", "random"])
 @pytest.mark.parametrize("block", [65536, 4 << 20, 300_001])
-def test_decompress_kinds_and_sizes(gpu, oracle, kind, block):
+def test_decompress_kinds_and_sizes(gpu, oracle, kind, block, decoder):
     """The hot decoder on every corpus kind at 64 KiB, 4 MiB and an odd
     block size: long matches (markup: ml > 16 on 70 % of sequences), offsets
     around the LDS ring's reach, runs and incompressible blocks, positions
@@ -288,9 +303,71 @@ def test_decompress_kinds_and_sizes(gpu, oracle, kind, block):
     raw = _synth.blocks(n * block // 65536 + 1, kind, seed=31).tobytes()
     blocks = [raw[i * block:(i + 1) * block] for i in range(n)]
     comp = [oracle.compress(b) for b in blocks]
-    got = gpu_decompress(comp, [block] * n, gpu)
+    got = gpu_decompress(comp, [block] * n, gpu, decoder)
     for (st, out), b in zip(got, blocks):
         assert st == len(b) and out == b
+
+
+def _offset0_block(lit, ml):
+    """A block whose one match has offset 0 (LZ4_decompress_safe v1.9.4 zero-fills
+    it) followed by 5 final literals."""
+    seq = bytes([(len(lit) << 4) | (ml - 4)]) + lit + b"\x00\x00"
+    return seq + bytes([5 << 4]) + b"tail!"
+
+
+@pytest.mark.parametrize("decoder", ["auto", "lane"])
+def test_decompress_large_batch_edges(gpu, oracle, corpus, decoder):
+    """A batch above the small-batch switch-over (98 304 blocks), so the
+    default dispatch runs the large-batch decoder, with every edge case of the
+    small tests embedded: the golden decode vectors with their capacities,
+    3 000 mutated / truncated blocks, random garbage, ragged sizes 0..65536,
+    offset-0 blocks and capacities below the size.  Statuses and bytes must
+    equal the oracle's (lz4libs/lz4.c:1936-2339)."""
+    import json
+    import os
+    from conftest import GOLDEN
+    blocks, ragged = corpus
+    cases, caps = [], []
+    man = json.load(open(os.path.join(GOLDEN, "manifest.json")))
+    arr = np.load(os.path.join(GOLDEN, "golden.npz"), allow_pickle=False)
+    for e in man["decompress"]:
+        cases.append(arr[e["key"]].tobytes())
+        caps.append(e["cap"])
+    mc, mcap = malformed_cases(oracle, blocks)
+    cases += mc
+    caps += mcap
+    rng = np.random.default_rng(9)
+    for _ in range(1000):
+        cases.append(rng.integers(0, 256, size=int(rng.integers(1, 300)), dtype=np.uint8).tobytes())
+        caps.append(int(rng.integers(0, 5000)))
+    for r in ragged + blocks[:8]:
+        c = oracle.compress(r)
+        for cap in {len(r), max(0, len(r) - 1), len(r) + 7, max(0, len(r) - 70)}:
+            cases.append(c)
+            caps.append(cap)
+    for k in range(64):
+        b = _offset0_block(bytes([65 + k % 26]) * (k % 13), 4 + k % 11)
+        cases.append(b)
+        caps.append(k % 13 + 4 + k % 11 + 5 + (k % 3) * 40)
+    # fill with small valid blocks (pieces of the corpus) past the switch-over
+    pool = [oracle.compress(blocks[i % len(blocks)][(i * 97) % 60000:(i * 97) % 60000 + 64 + i % 700])
+            for i in range(512)]
+    want_len = [64 + i % 700 for i in range(512)]
+    i = 0
+    while len(cases) < 100_000:
+        cases.append(pool[i % 512])
+        caps.append(want_len[i % 512])
+        i += 1
+    res = gpu_decompress(cases, caps, gpu, decoder)
+    memo = {}
+    for i, (s, out) in enumerate(res):
+        key = (cases[i], caps[i])
+        want = memo.get(key)
+        if want is None:
+            want = memo[key] = oracle.decompress(cases[i], caps[i])
+        assert s == want[0], (i, s, want[0], caps[i])
+        if s >= 0:
+            assert out == want[1], i
 
 
 def test_host_single_block_functions(gpu, oracle, corpus):
