@@ -68,12 +68,13 @@ __device__ __forceinline__ int32_t row_excl_min(int32_t v) {
     return x;
 }
 
-// Exactly k bytes (k >= 16: 16) of v at LDS address p.
+// Exactly k bytes (k >= 16: 16; k <= 0: none) of v at LDS address p.
 __device__ __forceinline__ void lds_put(lds_u8* p, u32x4 v, int32_t k) {
     if (k >= 16) {
         lds_st16(p, v);
         return;
     }
+    if (k <= 0) return;
     uint32_t o = 0;
     if (k & 8) {
         const uint64_t x = ((uint64_t)v.y << 32) | v.x;
@@ -120,53 +121,21 @@ __device__ __forceinline__ void gbl_put(uint8_t* p, u32x4 v, int32_t k) {
 }
 
 // ------------------------------------------------------------ 1. the parse
-// Lane state of rows_parse_kernel.  The compressed block is read through a
-// 64-byte LDS window [ib, ib + 64) refilled by 16-byte loads (zeros past
-// iend); recorded lengths are staged 64 at a time in LDS and leave for HBM as
-// whole 64-byte chunks.
-constexpr int kPWin = 64;
-constexpr int kPStage = 64;
-
-struct Parser {
-    const uint8_t* s;
-    lds_u8* win;
-    int32_t iend, ib;
-};
-
-__device__ __forceinline__ uint32_t p_byte(const Parser& P, int32_t x) {
-    const int32_t d = x - P.ib;
-    return (d >= 0 && d < kPWin) ? (uint32_t)P.win[d] : (uint32_t)P.s[x];
-}
-
-// make the window cover [ip, ip + 32)
-__device__ __forceinline__ void p_sync(Parser& P, int32_t ip) {
-    const int32_t d = ip - P.ib;
-    if (d < 32) return;
-    const bool shift = d < 64;
-    const int32_t nb = shift ? P.ib + 32 : (ip & ~15);
-    const int32_t first = shift ? nb + 32 : nb;
-    u32x4 k0 = u32x4{0, 0, 0, 0}, k1 = k0;
-    if (shift) {
-        k0 = lds_ld16(P.win + 32);
-        k1 = lds_ld16(P.win + 48);
-    }
-    u32x4 v[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int32_t x = nb + 16 * k;
-        v[k] = u32x4{0, 0, 0, 0};
-        if (x >= first) v[k] = x + 16 <= P.iend ? ld16(P.s + x) : ld16_guarded(P.s + x, P.iend - x);
-    }
-    if (shift) {
-        lds_st16(P.win, k0);
-        lds_st16(P.win + 16, k1);
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        if (nb + 16 * k >= first) lds_st16(P.win + 16 * k, v[k]);
-    }
-    P.ib = nb;
-}
+// One lane per block.  The compressed block is read through a 128-byte LDS
+// window per lane.  A lane parses sequences out of its window until it needs
+// bytes beyond it; the wave then refills the windows of all lanes waiting,
+// with all their loads in flight at once (one memory round trip per ~20
+// sequences per lane instead of one per refill), and parsing resumes.  A
+// sequence whose literal skips past the window is split: the token and
+// literal length are parsed first, the offset and match length after the
+// window moves to them.  Recorded lengths are staged 32 at a time in LDS and
+// leave for HBM as whole 32-byte chunks.
+constexpr int kPW = 128;                // window bytes
+constexpr int kPWS = kPW + 16;          // window stride
+constexpr int kPStage = 32;
+#ifndef LZ4M_PARSE_MIN_ACTIVE
+#define LZ4M_PARSE_MIN_ACTIVE 16        // refill once fewer lanes than this can still parse
+#endif
 
 __global__ __launch_bounds__(256) void rows_parse_kernel(const uint8_t* __restrict__ src,
                                                          const int64_t* __restrict__ src_off,
@@ -174,52 +143,54 @@ __global__ __launch_bounds__(256) void rows_parse_kernel(const uint8_t* __restri
                                                          const int32_t* __restrict__ dst_cap, int64_t n,
                                                          RowMeta* __restrict__ meta, uint8_t* __restrict__ lens,
                                                          int64_t lens_cap, unsigned long long* __restrict__ ctr) {
-    __shared__ __attribute__((aligned(16))) uint8_t wins[256 * kPWin];
+    __shared__ __attribute__((aligned(16))) uint8_t wins[256 * kPWS];
     __shared__ __attribute__((aligned(16))) uint8_t stgs[256 * kPStage];
     const uint32_t lane = lane_id();
+    lds_u8* W = (lds_u8*)(wins + threadIdx.x * kPWS);
     lds_u8* stg = (lds_u8*)(stgs + threadIdx.x * kPStage);
-    Parser P;
-    P.win = (lds_u8*)(wins + threadIdx.x * kPWin);
-    P.s = nullptr;
-    P.iend = 0;
-    P.ib = 0;
+    const uint8_t* s = nullptr;
     int64_t idx = -1, loff = 0;
-    int32_t oend = 0, ip = 0, op = 0, k = 0;
-    bool live = false, more = true;
+    int32_t iend = 0, oend = 0, ip = 0, op = 0, k = 0, ib = 0;
+    // a sequence split at its offset: po >= 0 is the offset position, ptok /
+    // plit the token and literal length already parsed
+    int32_t po = -1, plit = 0;
+    uint32_t ptok = 0;
+    int32_t want = 0;   // window wanted at this position (need)
+    bool live = false, need = false, more = true;
     while (true) {
         if (more) {
             // idle lanes take the next blocks: one queue atomic and one
             // length-space atomic per wave refill
-            const uint64_t need = __ballot(!live);
-            if (need != 0) {
-                const int first = __builtin_ctzll(need);
-                const uint32_t cnt = (uint32_t)__popcll(need);
+            const uint64_t idle = __ballot(!live);
+            if (idle != 0 && (uint32_t)__popcll(idle) >= LZ4M_PARSE_MIN_ACTIVE / 2) {
+                const int first = __builtin_ctzll(idle);
+                const uint32_t cnt = (uint32_t)__popcll(idle);
                 unsigned long long qb = 0;
                 if ((int)lane == first) qb = atomicAdd(&ctr[0], (unsigned long long)cnt);
                 qb = (unsigned long long)readlane64((int64_t)qb, first);
                 if (qb + cnt >= (unsigned long long)n) more = false;
-                int64_t want = 0;
+                int64_t wantb = 0;
                 bool fresh = false;
                 if (!live) {
-                    const uint64_t below = lane == 0 ? 0 : (need & (~0ull >> (64 - lane)));
+                    const uint64_t below = lane == 0 ? 0 : (idle & (~0ull >> (64 - lane)));
                     idx = (int64_t)(qb + (unsigned long long)__popcll(below));
                     if (idx < n) {
-                        P.s = src + src_off[idx];
-                        P.iend = src_len[idx];
+                        s = src + src_off[idx];
+                        iend = src_len[idx];
                         oend = dst_cap[idx];
                         ip = op = k = 0;
-                        P.ib = -2 * kPWin;
-                        if (oend >= 64 && P.iend > 0) {   // else: no fast loop (lz4.c:1990-1993) or a special case
+                        po = -1;
+                        if (oend >= 64 && iend > 0) {   // else: no fast loop (lz4.c:1990-1993) or a special case
                             // a good sequence takes >= 3 input and >= 4 output bytes
-                            const int32_t a = P.iend / 3, b = oend / 4;
-                            want = (int64_t)(a < b ? a : b) + 1;
+                            const int32_t a = iend / 3, b = oend / 4;
+                            wantb = (int64_t)(a < b ? a : b) + 1;
                             fresh = true;
                         } else {
                             meta[idx] = RowMeta{0, 0, 0, 0, 0, 0};
                         }
                     }
                 }
-                int64_t incl = want;
+                int64_t incl = wantb;
 #pragma unroll
                 for (int dd = 1; dd < 64; dd <<= 1) {
                     const int64_t t = __shfl_up(incl, dd);
@@ -232,11 +203,13 @@ __global__ __launch_bounds__(256) void rows_parse_kernel(const uint8_t* __restri
                     abase = readlane64(abase, 0);
                 }
                 if (fresh) {
-                    loff = abase + incl - want;
-                    if (loff + want > lens_cap) {
+                    loff = abase + incl - wantb;
+                    if (loff + wantb > lens_cap) {
                         meta[idx] = RowMeta{0, 0, 0, 0, 0, 0};   // no room: the finisher decodes the whole block
                     } else {
                         live = true;
+                        need = true;
+                        want = 0;
                     }
                 }
             }
@@ -245,42 +218,73 @@ __global__ __launch_bounds__(256) void rows_parse_kernel(const uint8_t* __restri
             if (more) continue;
             break;
         }
-        if (live) {
-            // one sequence, with the reference fast loop's tests (lz4.c:2004-2086)
-            p_sync(P, ip);
-            const int32_t iend = P.iend;
-            const uint32_t tok = p_byte(P, ip);
-            int64_t lit = tok >> 4;
-            int32_t q = ip + 1;
-            bool good = true;
-            if (lit == 15) {   // read_variable_length(&ip, iend - 15, 1), lz4.c:1903-1928
-                if (q >= iend - 15) {
-                    good = false;
-                } else {
-                    uint32_t b;
-                    do {
-                        b = p_byte(P, q);
-                        ++q;
-                        lit += b;
-                        if (q > iend - 15) good = false;
-                    } while (good && b == 255);
-                    if (good && (op + lit > oend - 32 || q + lit > iend - 32)) good = false;   // :2016-2027
-                }
-            } else if (q > iend - 17) {   // :2034
-                good = false;
+        // refill every waiting window at once
+        if (live && need) {
+            const int32_t nb = want & ~15;
+            u32x4 v[kPW / 16];
+#pragma unroll
+            for (int c = 0; c < kPW / 16; ++c) {
+                const int32_t x = nb + 16 * c;
+                v[c] = x + 16 <= iend ? ld16(s + x) : ld16_guarded(s + x, iend - x);
             }
-            int32_t pe = 0;
-            int64_t ml = 0;
-            uint32_t off = 0;
+#pragma unroll
+            for (int c = 0; c < kPW / 16; ++c) lds_st16(W + 16 * c, v[c]);
+            ib = nb;
+            need = false;
+        }
+        // parse until too few lanes can go on
+        while (true) {
+            const bool go = live && !need;
+            const uint64_t gm = __ballot(go);
+            if (gm == 0 || (uint32_t)__popcll(gm) < (uint32_t)min(LZ4M_PARSE_MIN_ACTIVE, __popcll(__ballot(live))))
+                break;
+            if (!go) continue;
+            // one sequence, with the reference fast loop's tests (lz4.c:2004-2086)
+            bool good = true;
+            if (po < 0) {
+                if (ip + 16 > ib + kPW) {   // token + 15 bytes must be in the window
+                    need = true;
+                    want = ip;
+                    continue;
+                }
+                const uint32_t tok = W[ip - ib];
+                int64_t lit = tok >> 4;
+                int32_t q = ip + 1;
+                if (lit == 15) {   // read_variable_length(&ip, iend - 15, 1), lz4.c:1903-1928
+                    if (q >= iend - 15) {
+                        good = false;
+                    } else {
+                        uint32_t b;
+                        do {
+                            b = q - ib < kPW ? (uint32_t)W[q - ib] : (uint32_t)s[q];
+                            ++q;
+                            lit += b;
+                            if (q > iend - 15) good = false;
+                        } while (good && b == 255);
+                        if (good && (op + lit > oend - 32 || q + lit > iend - 32)) good = false;   // :2016-2027
+                    }
+                } else if (q > iend - 17) {   // :2034
+                    good = false;
+                }
+                if (good) {
+                    po = q + (int32_t)lit;
+                    plit = (int32_t)lit;
+                    ptok = tok;
+                }
+            }
             if (good) {
-                const int32_t po = q + (int32_t)lit;
-                off = p_byte(P, po) | (p_byte(P, po + 1) << 8);
-                pe = po + 2;
-                ml = tok & 15;
+                if (po + 3 > ib + kPW) {   // the offset and first length byte must be in the window
+                    need = true;
+                    want = po;
+                    continue;
+                }
+                const uint32_t off = (uint32_t)W[po - ib] | ((uint32_t)W[po + 1 - ib] << 8);
+                int32_t pe = po + 2;
+                int64_t ml = ptok & 15;
                 if (ml == 15) {   // read_variable_length(&ip, iend - 4, 0)
                     uint32_t b;
                     do {
-                        b = p_byte(P, pe);
+                        b = pe - ib < kPW ? (uint32_t)W[pe - ib] : (uint32_t)s[pe];
                         ++pe;
                         ml += b;
                         if (pe > iend - 4) good = false;
@@ -289,33 +293,40 @@ __global__ __launch_bounds__(256) void rows_parse_kernel(const uint8_t* __restri
                 ml += 4;
                 // offset 0 and offsets before the block start go to the exact
                 // path (lz4.c:2071, :2081); so do matches reaching oend - 64 (:2073, :2076)
-                if (good && (off == 0 || (int64_t)off > op + lit || op + lit + ml >= (int64_t)oend - 64)) good = false;
-            }
-            if (good) {
-                const int32_t adv = pe - ip;
-                stg[k & 63] = (uint8_t)(adv < 255 ? adv : 255);
-                if ((k & 63) == 63) {
-                    uint8_t* o = lens + loff + (k & ~63);
+                if (good && (off == 0 || (int64_t)off > (int64_t)op + plit ||
+                             (int64_t)op + plit + ml >= (int64_t)oend - 64))
+                    good = false;
+                if (good) {
+                    const int32_t adv = pe - ip;
+                    stg[k & (kPStage - 1)] = (uint8_t)(adv < 255 ? adv : 255);
+                    if ((k & (kPStage - 1)) == kPStage - 1) {
+                        uint8_t* o = lens + loff + (k & ~(kPStage - 1));
 #pragma unroll
-                    for (int c = 0; c < 4; ++c) st16(o + 16 * c, lds_ld16(stg + 16 * c));
+                        for (int c = 0; c < kPStage / 16; ++c) st16(o + 16 * c, lds_ld16(stg + 16 * c));
+                    }
+                    ip = pe;
+                    op += plit + (int32_t)ml;
+                    ++k;
+                    po = -1;
+                    continue;
                 }
-                ip = pe;
-                op += (int32_t)(lit + ml);
-                ++k;
-            } else {
-                const int32_t rest = k & 63;
-                uint8_t* o = lens + loff + (k & ~63);
-                for (int c = 0; c < rest; c += 16) gbl_put(o + c, lds_ld16(stg + c), rest - c);
-                meta[idx] = RowMeta{loff, k, ip, op, 0, 0};
-                live = false;
             }
+            // the first sequence that is not good: the finisher resumes here
+            const int32_t rest = k & (kPStage - 1);
+            uint8_t* o = lens + loff + (k & ~(kPStage - 1));
+            for (int c = 0; c < rest; c += 16) gbl_put(o + c, lds_ld16(stg + c), rest - c);
+            meta[idx] = RowMeta{loff, k, ip, op, 0, 0};
+            live = false;
         }
     }
 }
 
 // ------------------------------------------------------- 2. row execution
-// Per row: output [base, base + kRowsH) of the block in LDS (history), the
-// round's compressed bytes [ib, ib + 256) in an LDS window.
+// Per row: output [base, base + kRowsH) of the block in LDS (the history).
+// Lane jj reads its sequence straight from HBM: 32 bytes at its start, which
+// the row knows from the recorded lengths (row prefix sum).  The lengths and
+// the 32 bytes of the NEXT round are requested while this round copies, so a
+// round waits on at most one memory round trip (its far match sources).
 #ifndef LZ4M_ROWS_H
 #define LZ4M_ROWS_H 2048
 #endif
@@ -323,8 +334,6 @@ constexpr int32_t kRowsH = LZ4M_ROWS_H;
 constexpr int32_t kRowsHS = kRowsH + 32;   // buffer stride (16-byte reads past the end stay inside)
 constexpr int32_t kRowsKeep = kRowsH / 2;   // history kept on a rebase
 constexpr int32_t kRowsRoom = 512;          // rebase when less room than this is left
-constexpr int32_t kRowsWin = 256;
-constexpr int32_t kRowsWS = kRowsWin + 16;
 
 // Row-cooperative exact copies in HBM (16 lanes, lane j = jj).
 __device__ __forceinline__ void row_copy_literal(uint8_t* d, const uint8_t* s, int32_t len, int32_t jj) {
@@ -349,6 +358,23 @@ __device__ __forceinline__ void row_copy_match(uint8_t* d, int32_t off, int32_t 
     for (int32_t pos = step * jj; pos < len; pos += step * 16) gbl_put(d + pos, pat, len - pos);
 }
 
+// 32 bytes of block input at t (bytes at or past iend read as zero)
+__device__ __forceinline__ void load32(const uint8_t* s, int32_t t, int32_t iend, bool valid, u32x4& a, u32x4& b) {
+    a = u32x4{0, 0, 0, 0};
+    b = a;
+    if (!valid) return;
+    a = t + 16 <= iend ? ld16(s + t) : ld16_guarded(s + t, iend - t);
+    b = t + 32 <= iend ? ld16(s + t + 16) : ld16_guarded(s + t + 16, iend - t - 16);
+}
+
+// the 4 bytes at k (0..28) of the 32-byte window a|b
+__device__ __forceinline__ uint32_t dword32(u32x4 a, u32x4 b, uint32_t k) {
+    const uint32_t q = k >> 2;
+    const uint32_t lo = q == 0 ? a.x : q == 1 ? a.y : q == 2 ? a.z : q == 3 ? a.w : q == 4 ? b.x : q == 5 ? b.y : q == 6 ? b.z : b.w;
+    const uint32_t hi = q == 0 ? a.y : q == 1 ? a.z : q == 2 ? a.w : q == 3 ? b.x : q == 4 ? b.y : q == 5 ? b.z : q == 6 ? b.w : 0u;
+    return __builtin_amdgcn_alignbyte(hi, lo, k & 3);
+}
+
 __global__ __launch_bounds__(64) void rows_exec_kernel(const uint8_t* __restrict__ src,
                                                        const int64_t* __restrict__ src_off,
                                                        const int32_t* __restrict__ src_len, uint8_t* dst,
@@ -357,17 +383,19 @@ __global__ __launch_bounds__(64) void rows_exec_kernel(const uint8_t* __restrict
                                                        const uint8_t* __restrict__ lens, int64_t n,
                                                        unsigned long long* __restrict__ ctr) {
     __shared__ __attribute__((aligned(16))) uint8_t hists[4 * kRowsHS];
-    __shared__ __attribute__((aligned(16))) uint8_t wins[4 * kRowsWS];
     const uint32_t lane = threadIdx.x;
     const int32_t jj = (int32_t)(lane & 15), r = (int32_t)(lane >> 4);
     lds_u8* HB = (lds_u8*)(hists + r * kRowsHS);
-    lds_u8* IN = (lds_u8*)(wins + r * kRowsWS);
     // row state (uniform across the row's 16 lanes)
     const uint8_t* s = nullptr;
     uint8_t* d = nullptr;
     const uint8_t* dl = nullptr;
     int32_t iend = 0, nseq = 0, k0 = 0, ip = 0, op = 0, base = 0, F = 0;
-    bool have = false;
+    bool have = false, pf = false;
+    // this round's inputs (valid when pf): length dc, start tc, bytes wa|wb;
+    // dn = the next round's length
+    int32_t dc = 0, tc = 0, dn = 0;
+    u32x4 wa = u32x4{0, 0, 0, 0}, wb = wa;
     while (true) {
         if (!have) {
             unsigned long long b = 0;
@@ -385,6 +413,7 @@ __global__ __launch_bounds__(64) void rows_exec_kernel(const uint8_t* __restrict
             nseq = mt.nseq;
             k0 = ip = op = base = F = 0;
             have = true;
+            pf = false;
         }
         // keep kRowsRoom bytes of room; never drop unflushed bytes (F >= op - 15)
         if (op - base > kRowsH - kRowsRoom) {
@@ -395,50 +424,63 @@ __global__ __launch_bounds__(64) void rows_exec_kernel(const uint8_t* __restrict
         // ---- the round: lane jj takes sequence k0 + jj
         const int32_t k = k0 + jj;
         const bool act = k < nseq;
-        const int32_t dlt = act ? (int32_t)dl[k] : 0;
-        const int32_t t = ip + row_incl_sum(dlt) - dlt;   // its start
-        const int32_t ib = ip & ~15;
-        {
-            const int32_t x = ib + 16 * jj;
-            const u32x4 v = x + 16 <= iend ? ld16(s + x) : ld16_guarded(s + x, iend - x);
-            lds_st16(IN + 16 * jj, v);
+        if (!pf) {   // block start, or the last round stopped early: load now
+            dc = act ? (int32_t)dl[k] : 0;
+            tc = ip + row_incl_sum(dc) - dc;
+            load32(s, tc, iend, act, wa, wb);
+            dn = k + 16 < nseq ? (int32_t)dl[k + 16] : 0;
         }
-        const bool inwin = act && dlt != 255 && t + dlt <= ib + kRowsWin;
-        const int32_t tr = inwin ? t - ib : 0;
-        const u32x4 w = lds_ld16(IN + tr);
-        const uint32_t tok = w.x & 0xFFu;
-        int32_t lit = (int32_t)(tok >> 4), lp = tr + 1;
-        if (inwin && lit == 15) {
-            uint32_t b;
-            do {
-                b = IN[lp];
-                ++lp;
-                lit += (int32_t)b;
-            } while (b == 255);
+        const int32_t t = tc, dlt = dc;
+        const bool esc = dlt == 255;   // length >= 255: the parse left it to be re-parsed
+        const uint32_t tok = wa.x & 0xFFu;
+        int32_t lit = (int32_t)(tok >> 4), lp = 1;
+        if (lit == 15) {
+            lit += (int32_t)byte_of(wa, 1);   // one extra byte unless the length escaped
+            lp = 2;
         }
-        int32_t off, ml = (int32_t)(tok & 15u);
-        int32_t pe = lp + lit + 2;
+        const int32_t po = lp + lit;
+        int32_t off = 0, ml = (int32_t)(tok & 15u);
+        bool slow = false;
         if (lit <= 12) {
-            off = (int32_t)(window_dword(w, (uint32_t)(1 + lit)) & 0xFFFFu);
+            off = (int32_t)(window_dword(wa, (uint32_t)po) & 0xFFFFu);
+            if (ml == 15) {
+                const int32_t e = (int32_t)byte_of(wa, po + 2);
+                ml += e;
+                slow = e == 255;
+            }
+        } else if (po + 3 <= 32) {
+            off = (int32_t)(dword32(wa, wb, (uint32_t)po) & 0xFFFFu);
+            if (ml == 15) {
+                const int32_t e = (int32_t)((dword32(wa, wb, (uint32_t)(po + 2 < 28 ? po + 2 : 28)) >> (8 * (po + 2 - (po + 2 < 28 ? po + 2 : 28)))) & 0xFFu);
+                ml += e;
+                slow = e == 255;
+            }
         } else {
-            off = (int32_t)IN[lp + lit] | ((int32_t)IN[lp + lit + 1] << 8);
+            slow = true;
         }
-        if (inwin && ml == 15) {
-            uint32_t b;
-            do {
-                b = IN[pe];
-                ++pe;
-                ml += (int32_t)b;
-            } while (b == 255);
+        if (slow && act && !esc) {   // a long match length or the offset past 32 bytes: from HBM
+            const uint8_t* q = s + t;
+            off = (int32_t)q[po] | ((int32_t)q[po + 1] << 8);
+            ml = (int32_t)(tok & 15u);
+            if (ml == 15) {
+                int32_t pe = po + 2;
+                uint32_t b;
+                do {
+                    b = q[pe];
+                    ++pe;
+                    ml += (int32_t)b;
+                } while (b == 255 && pe < iend - t);
+            }
         }
         ml += 4;
-        const int32_t len = inwin ? lit + ml : 0;
+        const int32_t len = act && !esc ? lit + ml : 0;
         const int32_t o = op + row_incl_sum(len) - len;
         const int32_t m = o + lit, mend = m + ml;
-        const bool ok = inwin && mend <= base + kRowsH;
+        const bool ok = act && !esc && mend <= base + kRowsH;
         const uint32_t rb = (uint32_t)(__ballot(!ok) >> (16 * r)) & 0xFFFFu;
         const int32_t use = rb ? __builtin_ctz(rb) : 16;
         if (use == 0) {
+            pf = false;
             if (k0 >= nseq) {   // the block's good prefix is done: flush the rest exactly
                 for (int32_t c = F + 16 * jj; c < op; c += 256) gbl_put(d + c, lds_ld16(HB + (c - base)), op - c);
                 have = false;
@@ -484,16 +526,40 @@ __global__ __launch_bounds__(64) void rows_exec_kernel(const uint8_t* __restrict
             continue;
         }
         const bool u = jj < use;
+        const int32_t opn = op + row_last(row_incl_sum(u ? len : 0));
+        const int32_t ipn = ip + row_last(row_incl_sum(u ? dlt : 0));
+        // the next round's lengths and bytes, requested now (valid if this
+        // round takes all 16 sequences)
+        const bool pfn = use == 16;
+        int32_t tn = 0, dn2 = 0;
+        u32x4 na = u32x4{0, 0, 0, 0}, nb2 = na;
+        if (pfn) {
+            const int32_t kn = k0 + 16 + jj;
+            tn = ipn + row_incl_sum(dn) - dn;
+            load32(s, tn, iend, kn < nseq, na, nb2);
+            dn2 = kn + 16 < nseq ? (int32_t)dl[kn + 16] : 0;
+        }
         const int32_t s0 = m - off;
-        // sources older than the buffer: the first 16 bytes are requested now
+        // sources older than the buffer: their first 32 bytes are requested now
         const bool far = u && s0 < base;
-        u32x4 pre = u32x4{0, 0, 0, 0};
-        if (far) pre = ld16(d + s0);
+        u32x4 pre0 = u32x4{0, 0, 0, 0}, pre1 = pre0;
+        if (far) {
+            pre0 = ld16(d + s0);
+            if (ml > 16) pre1 = ld16(d + s0 + 16);
+        }
         if (u && lit > 0) {
             if (lit <= 12) {
-                lds_put(HB + (o - base), window_shift1(w), lit);
-            } else {
-                for (int32_t i = 0; i < lit; i += 16) lds_put(HB + (o - base + i), lds_ld16(IN + lp + i), lit - i);
+                lds_put(HB + (o - base), window_shift1(wa), lit);
+            } else if (lp + lit <= 32) {
+                const uint32_t sh = (uint32_t)lp;
+                const u32x4 x0 = u32x4{__builtin_amdgcn_alignbyte(wa.y, wa.x, sh), __builtin_amdgcn_alignbyte(wa.z, wa.y, sh),
+                                       __builtin_amdgcn_alignbyte(wa.w, wa.z, sh), __builtin_amdgcn_alignbyte(wb.x, wa.w, sh)};
+                const u32x4 x1 = u32x4{__builtin_amdgcn_alignbyte(wb.y, wb.x, sh), __builtin_amdgcn_alignbyte(wb.z, wb.y, sh),
+                                       __builtin_amdgcn_alignbyte(wb.w, wb.z, sh), __builtin_amdgcn_alignbyte(0u, wb.w, sh)};
+                lds_put(HB + (o - base), x0, lit);
+                if (lit > 16) lds_put(HB + (o - base + 16), x1, lit - 16);
+            } else {   // a literal beyond the 32 bytes: from HBM (inside the block: good)
+                for (int32_t i = 0; i < lit; i += 16) lds_put(HB + (o - base + i), ld16(s + t + lp + i), lit - i);
             }
         }
         // readiness passes: a match is copied once no earlier pending match of
@@ -509,7 +575,8 @@ __global__ __launch_bounds__(64) void rows_exec_kernel(const uint8_t* __restrict
                     for (int32_t i = 0; i < ml; i += 16) {
                         const int32_t sp = s0 + i;
                         // sp < base: flushed (F >= base + kRowsKeep - 16)
-                        const u32x4 v = (i == 0 && far) ? pre : sp >= base ? lds_ld16(HB + (sp - base)) : ld16(d + sp);
+                        const u32x4 v = (far && i < 32) ? (i == 0 ? pre0 : pre1)
+                                                        : sp >= base ? lds_ld16(HB + (sp - base)) : ld16(d + sp);
                         lds_put(HB + (m - base + i), v, ml - i);
                     }
                 } else {   // s0 >= base: m - base >= off here
@@ -520,8 +587,14 @@ __global__ __launch_bounds__(64) void rows_exec_kernel(const uint8_t* __restrict
             }
             pend = pend && !ready;
         }
-        const int32_t opn = op + row_last(row_incl_sum(u ? len : 0));
-        const int32_t ipn = ip + row_last(row_incl_sum(u ? dlt : 0));
+        if (pfn) {
+            dc = dn;
+            tc = tn;
+            wa = na;
+            wb = nb2;
+            dn = dn2;
+        }
+        pf = pfn;
         for (int32_t c = F + 16 * jj; c + 16 <= opn; c += 256) st16(d + c, lds_ld16(HB + (c - base)));
         F += (opn - F) & ~15;
         op = opn;
