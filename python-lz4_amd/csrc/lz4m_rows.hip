@@ -36,6 +36,21 @@
 
 namespace lz4m {
 
+// LZ4M_ROWS_PROF (diagnostic builds only, tools/prof_rows.sh): per-phase
+// wave-cycle sums and event counts of the two kernels, read with lz4m_rows_prof.
+#ifdef LZ4M_ROWS_PROF
+__device__ unsigned long long g_rows_prof[32];
+#define RP_DECL uint64_t rp[32] = {0}; uint64_t rp_t = clock64();
+#define RP_MARK(i) do { const uint64_t _t = clock64(); rp[i] += _t - rp_t; rp_t = _t; } while (0)
+#define RP_COUNT(i, x) rp[i] += (uint64_t)(x)
+#define RP_FLUSH(a, b) do { if (lane == 0) for (int _i = (a); _i < (b); ++_i) atomicAdd(&g_rows_prof[_i], (unsigned long long)rp[_i]); } while (0)
+#else
+#define RP_DECL
+#define RP_MARK(i) do {} while (0)
+#define RP_COUNT(i, x) do {} while (0)
+#define RP_FLUSH(a, b) do {} while (0)
+#endif
+
 // ------------------------------------------------------------- row helpers
 // A row = 16 consecutive lanes; DPP row_shr stays inside a row and
 // row_newbcast:n (gfx90a+) broadcasts lane n of each row to the whole row.
@@ -68,6 +83,24 @@ __device__ __forceinline__ int32_t row_excl_min(int32_t v) {
     return x;
 }
 
+// Two exclusive max-scans over the row at once (values >= 0, 0 = none):
+// max of a and of b over the lanes below (0 for lane 0).  Identity 0 lets
+// each step fold into one v_max_i32_dpp; the two chains interleave.
+__device__ __forceinline__ void row_excl_max2(int32_t a, int32_t b, int32_t& xa, int32_t& xb) {
+    int32_t x = __builtin_amdgcn_update_dpp(0, a, 0x111, 0xF, 0xF, false);
+    int32_t y = __builtin_amdgcn_update_dpp(0, b, 0x111, 0xF, 0xF, false);
+    x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, false));
+    y = max(y, __builtin_amdgcn_update_dpp(0, y, 0x111, 0xF, 0xF, false));
+    x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, false));
+    y = max(y, __builtin_amdgcn_update_dpp(0, y, 0x112, 0xF, 0xF, false));
+    x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, false));
+    y = max(y, __builtin_amdgcn_update_dpp(0, y, 0x114, 0xF, 0xF, false));
+    x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, false));
+    y = max(y, __builtin_amdgcn_update_dpp(0, y, 0x118, 0xF, 0xF, false));
+    xa = x;
+    xb = y;
+}
+
 // Exactly k bytes (k >= 16: 16; k <= 0: none) of v at LDS address p.
 __device__ __forceinline__ void lds_put(lds_u8* p, u32x4 v, int32_t k) {
     if (k >= 16) {
@@ -92,6 +125,24 @@ __device__ __forceinline__ void lds_put(lds_u8* p, u32x4 v, int32_t k) {
         o += 2;
     }
     if (k & 1) p[o] = (uint8_t)window_dword(v, o);
+}
+
+// Exactly k bytes (k >= 16: 16; k <= 0: none) of v at LDS address p,
+// without branches: the pieces that are not needed are written to the lane's
+// private 16-byte slot `dummy` instead (five LDS writes, ~15 VALU).
+__device__ __forceinline__ void lds_put_bf(lds_u8* p, lds_u8* dummy, u32x4 v, int32_t k) {
+    const bool full = k >= 16;
+    const uint32_t km = full ? 0u : (uint32_t)(k > 0 ? k : 0);
+    const bool b8 = (km & 8) != 0, b4 = (km & 4) != 0, b2 = (km & 2) != 0, b1 = (km & 1) != 0;
+    if (__any(full)) lds_st16(full ? p : dummy, v);   // 16-byte pieces are the rarer case
+    const uint64_t lo = ((uint64_t)v.y << 32) | v.x;
+    __builtin_memcpy((uint8_t*)(b8 ? p : dummy), &lo, 8);
+    const uint32_t d4 = b8 ? v.z : v.x;                       // dword at offset km & 8
+    __builtin_memcpy((uint8_t*)(b4 ? p + (km & 8) : dummy), &d4, 4);
+    const uint32_t d2 = b4 ? (b8 ? v.w : v.y) : d4;           // dword at offset km & 12
+    const uint16_t h2 = (uint16_t)d2;
+    __builtin_memcpy((uint8_t*)(b2 ? p + (km & 12) : dummy), &h2, 2);
+    *(b1 ? p + (km & 14) : dummy) = (uint8_t)(b2 ? (d2 >> 16) : d2);
 }
 
 // Exactly k bytes (k >= 16: 16) of v at global address p.
@@ -120,22 +171,50 @@ __device__ __forceinline__ void gbl_put(uint8_t* p, u32x4 v, int32_t k) {
     if (k & 1) p[o] = (uint8_t)window_dword(v, o);
 }
 
+// The 4 bytes at byte k (0..15) of w (bytes past 15 read as zero), with
+// selects only (no branches).
+__device__ __forceinline__ uint32_t dword_at(u32x4 w, uint32_t k) {
+    const bool b4 = (k & 4) != 0, b8 = (k & 8) != 0;
+    const uint32_t a0 = b4 ? w.y : w.x, a1 = b4 ? w.z : w.y, a2 = b4 ? w.w : w.z, a3 = b4 ? 0u : w.w;
+    const uint32_t lo = b8 ? a2 : a0, hi = b8 ? a3 : a1;
+    return __builtin_amdgcn_alignbyte(hi, lo, k & 3);
+}
+
 // ------------------------------------------------------------ 1. the parse
 // One lane per block.  The compressed block is read through a 128-byte LDS
-// window per lane.  A lane parses sequences out of its window until it needs
-// bytes beyond it; the wave then refills the windows of all lanes waiting,
-// with all their loads in flight at once (one memory round trip per ~20
-// sequences per lane instead of one per refill), and parsing resumes.  A
-// sequence whose literal skips past the window is split: the token and
-// literal length are parsed first, the offset and match length after the
-// window moves to them.  Recorded lengths are staged 32 at a time in LDS and
-// leave for HBM as whole 32-byte chunks.
-constexpr int kPW = 128;                // window bytes
-constexpr int kPWS = kPW + 16;          // window stride
-constexpr int kPStage = 32;
+// ring per lane holding stream bytes [wb, wb + 128) (wb a multiple of 64; a
+// 16-byte mirror after the ring keeps every 16-byte read contiguous), and the
+// next 64 bytes [wb + 128, wb + 192) are requested ahead into registers.  The
+// inner loop is the common sequence only -- literal <= 12 bytes, at most one
+// match-length byte, inside the ring, good -- as straight-line code (one
+// 16-byte LDS read, ~30 VALU).  A lane that meets anything else (the ring's
+// end, a longer literal or length, a full length stage, the block's end)
+// waits; once too few lanes can go on, the wave runs one general step: every
+// lane past the first half of its ring rotates the requested bytes in and
+// requests the next 64, waiting lanes parse one sequence with the general
+// parse.  Recorded lengths are staged in a 64-entry LDS ring per lane and
+// leave for HBM 32 at a time.
+constexpr int kPW = 128;                // ring bytes
+constexpr int kPWS = kPW + 16;          // ring + mirror
+constexpr int kPStage = 64;             // length ring (flushed in halves)
 #ifndef LZ4M_PARSE_MIN_ACTIVE
-#define LZ4M_PARSE_MIN_ACTIVE 16        // refill once fewer lanes than this can still parse
+#define LZ4M_PARSE_MIN_ACTIVE 40        // run the general step once fewer lanes than this can go on
 #endif
+
+// 64 stream bytes into ring half h (0: offsets 0-63, with the mirror; 1: 64-127)
+__device__ __forceinline__ void ring_put(lds_u8* W, int32_t h, const u32x4* v) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) lds_st16(W + 64 * h + 16 * c, v[c]);
+    if (h == 0) lds_st16(W + kPW, v[0]);
+}
+
+__device__ __forceinline__ void load64(const uint8_t* s, int32_t x, int32_t iend, u32x4* v) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int32_t y = x + 16 * c;
+        v[c] = y + 16 <= iend ? ld16(s + y) : ld16_guarded(s + y, iend - y);
+    }
+}
 
 __global__ __launch_bounds__(256) void rows_parse_kernel(const uint8_t* __restrict__ src,
                                                          const int64_t* __restrict__ src_off,
@@ -150,19 +229,17 @@ __global__ __launch_bounds__(256) void rows_parse_kernel(const uint8_t* __restri
     lds_u8* stg = (lds_u8*)(stgs + threadIdx.x * kPStage);
     const uint8_t* s = nullptr;
     int64_t idx = -1, loff = 0;
-    int32_t iend = 0, oend = 0, ip = 0, op = 0, k = 0, ib = 0;
-    // a sequence split at its offset: po >= 0 is the offset position, ptok /
-    // plit the token and literal length already parsed
-    int32_t po = -1, plit = 0;
-    uint32_t ptok = 0;
-    int32_t want = 0;   // window wanted at this position (need)
-    bool live = false, need = false, more = true;
+    int32_t iend = 0, oend = 0, ip = 0, op = 0, k = 0, kf = 0, wb = 0;
+    u32x4 pf[4];   // stream bytes [wb + 128, wb + 192), requested ahead
+    bool live = false, need = false, more = true, pfv = false;
+    RP_DECL
     while (true) {
+        RP_MARK(2);
         if (more) {
             // idle lanes take the next blocks: one queue atomic and one
             // length-space atomic per wave refill
             const uint64_t idle = __ballot(!live);
-            if (idle != 0 && (uint32_t)__popcll(idle) >= LZ4M_PARSE_MIN_ACTIVE / 2) {
+            if (idle != 0 && (uint32_t)__popcll(idle) >= 8u) {
                 const int first = __builtin_ctzll(idle);
                 const uint32_t cnt = (uint32_t)__popcll(idle);
                 unsigned long long qb = 0;
@@ -178,8 +255,9 @@ __global__ __launch_bounds__(256) void rows_parse_kernel(const uint8_t* __restri
                         s = src + src_off[idx];
                         iend = src_len[idx];
                         oend = dst_cap[idx];
-                        ip = op = k = 0;
-                        po = -1;
+                        ip = op = k = kf = 0;
+                        wb = -4 * kPW;
+                        pfv = false;
                         if (oend >= 64 && iend > 0) {   // else: no fast loop (lz4.c:1990-1993) or a special case
                             // a good sequence takes >= 3 input and >= 4 output bytes
                             const int32_t a = iend / 3, b = oend / 4;
@@ -209,82 +287,70 @@ __global__ __launch_bounds__(256) void rows_parse_kernel(const uint8_t* __restri
                     } else {
                         live = true;
                         need = true;
-                        want = 0;
                     }
                 }
             }
         }
+        RP_MARK(0);
         if (!__any(live)) {
             if (more) continue;
             break;
         }
-        // refill every waiting window at once
-        if (live && need) {
-            const int32_t nb = want & ~15;
-            u32x4 v[kPW / 16];
-#pragma unroll
-            for (int c = 0; c < kPW / 16; ++c) {
-                const int32_t x = nb + 16 * c;
-                v[c] = x + 16 <= iend ? ld16(s + x) : ld16_guarded(s + x, iend - x);
-            }
-#pragma unroll
-            for (int c = 0; c < kPW / 16; ++c) lds_st16(W + 16 * c, v[c]);
-            ib = nb;
-            need = false;
+        RP_COUNT(4, 1);
+        RP_COUNT(6, __popcll(__ballot(live && need)));
+        // ---- the general step
+        // rotate requested bytes in (every lane past the first half of its ring)
+        if (live && pfv && ip >= wb + 64) {
+            ring_put(W, (wb >> 6) & 1, pf);
+            wb += 64;
+            pfv = false;
         }
-        // parse until too few lanes can go on
-        while (true) {
-            const bool go = live && !need;
-            const uint64_t gm = __ballot(go);
-            if (gm == 0 || (uint32_t)__popcll(gm) < (uint32_t)min(LZ4M_PARSE_MIN_ACTIVE, __popcll(__ballot(live))))
-                break;
-            if (!go) continue;
-            // one sequence, with the reference fast loop's tests (lz4.c:2004-2086)
-            bool good = true;
-            if (po < 0) {
-                if (ip + 16 > ib + kPW) {   // token + 15 bytes must be in the window
-                    need = true;
-                    want = ip;
-                    continue;
-                }
-                const uint32_t tok = W[ip - ib];
-                int64_t lit = tok >> 4;
-                int32_t q = ip + 1;
-                if (lit == 15) {   // read_variable_length(&ip, iend - 15, 1), lz4.c:1903-1928
-                    if (q >= iend - 15) {
-                        good = false;
-                    } else {
-                        uint32_t b;
-                        do {
-                            b = q - ib < kPW ? (uint32_t)W[q - ib] : (uint32_t)s[q];
-                            ++q;
-                            lit += b;
-                            if (q > iend - 15) good = false;
-                        } while (good && b == 255);
-                        if (good && (op + lit > oend - 32 || q + lit > iend - 32)) good = false;   // :2016-2027
-                    }
-                } else if (q > iend - 17) {   // :2034
-                    good = false;
-                }
-                if (good) {
-                    po = q + (int32_t)lit;
-                    plit = (int32_t)lit;
-                    ptok = tok;
-                }
+        if (live && need) {
+            need = false;
+            if (ip + 32 > wb + kPW) {   // no bytes ahead (block start, a long literal): load the ring now
+                const int32_t nb = ip & ~63;
+                u32x4 v0[4], v1[4];
+                load64(s, nb, iend, v0);
+                load64(s, nb + 64, iend, v1);
+                ring_put(W, (nb >> 6) & 1, v0);
+                ring_put(W, ((nb >> 6) + 1) & 1, v1);
+                wb = nb;
+                pfv = false;
             }
-            if (good) {
-                if (po + 3 > ib + kPW) {   // the offset and first length byte must be in the window
-                    need = true;
-                    want = po;
-                    continue;
+            // one sequence, general parse with the reference fast loop's tests
+            // (lz4.c:2004-2086); bytes outside the ring come from HBM
+#define PB(x) ((x) - wb < kPW ? (uint32_t)W[(x) & (kPW - 1)] : (uint32_t)s[(x)])
+            bool good = true;
+            const uint32_t tok = PB(ip);
+            int64_t lit = tok >> 4;
+            int32_t q = ip + 1;
+            if (lit == 15) {   // read_variable_length(&ip, iend - 15, 1), lz4.c:1903-1928
+                if (q >= iend - 15) {
+                    good = false;
+                } else {
+                    uint32_t b;
+                    do {
+                        b = PB(q);
+                        ++q;
+                        lit += b;
+                        if (q > iend - 15) good = false;
+                    } while (good && b == 255);
+                    if (good && (op + lit > oend - 32 || q + lit > iend - 32)) good = false;   // :2016-2027
                 }
-                const uint32_t off = (uint32_t)W[po - ib] | ((uint32_t)W[po + 1 - ib] << 8);
-                int32_t pe = po + 2;
-                int64_t ml = ptok & 15;
+            } else if (q > iend - 17) {   // :2034
+                good = false;
+            }
+            int32_t pe = 0;
+            int64_t ml = 0;
+            if (good) {
+                const int32_t po = q + (int32_t)lit;
+                const uint32_t off = PB(po) | (PB(po + 1) << 8);
+                pe = po + 2;
+                ml = tok & 15;
                 if (ml == 15) {   // read_variable_length(&ip, iend - 4, 0)
                     uint32_t b;
                     do {
-                        b = pe - ib < kPW ? (uint32_t)W[pe - ib] : (uint32_t)s[pe];
+                        b = PB(pe);
                         ++pe;
                         ml += b;
                         if (pe > iend - 4) good = false;
@@ -293,32 +359,67 @@ __global__ __launch_bounds__(256) void rows_parse_kernel(const uint8_t* __restri
                 ml += 4;
                 // offset 0 and offsets before the block start go to the exact
                 // path (lz4.c:2071, :2081); so do matches reaching oend - 64 (:2073, :2076)
-                if (good && (off == 0 || (int64_t)off > (int64_t)op + plit ||
-                             (int64_t)op + plit + ml >= (int64_t)oend - 64))
+                if (good && (off == 0 || (int64_t)off > (int64_t)op + lit || (int64_t)op + lit + ml >= (int64_t)oend - 64))
                     good = false;
-                if (good) {
-                    const int32_t adv = pe - ip;
-                    stg[k & (kPStage - 1)] = (uint8_t)(adv < 255 ? adv : 255);
-                    if ((k & (kPStage - 1)) == kPStage - 1) {
-                        uint8_t* o = lens + loff + (k & ~(kPStage - 1));
-#pragma unroll
-                        for (int c = 0; c < kPStage / 16; ++c) st16(o + 16 * c, lds_ld16(stg + 16 * c));
-                    }
-                    ip = pe;
-                    op += plit + (int32_t)ml;
-                    ++k;
-                    po = -1;
-                    continue;
-                }
             }
-            // the first sequence that is not good: the finisher resumes here
-            const int32_t rest = k & (kPStage - 1);
-            uint8_t* o = lens + loff + (k & ~(kPStage - 1));
-            for (int c = 0; c < rest; c += 16) gbl_put(o + c, lds_ld16(stg + c), rest - c);
-            meta[idx] = RowMeta{loff, k, ip, op, 0, 0};
-            live = false;
+#undef PB
+            if (good) {
+                const int32_t adv = pe - ip;
+                stg[k & (kPStage - 1)] = (uint8_t)(adv < 255 ? adv : 255);
+                ip = pe;
+                op += (int32_t)(lit + ml);
+                ++k;
+            } else {   // the first sequence that is not good: the finisher resumes here
+                for (int32_t c = kf; c < k; c += 16) gbl_put(lens + loff + c, lds_ld16(stg + (c & 63)), k - c);
+                meta[idx] = RowMeta{loff, k, ip, op, 0, 0};
+                live = false;
+            }
+        }
+        // flush full halves of the length ring
+        if (live && k - kf >= 32) {
+            uint8_t* o = lens + loff + kf;
+            st16(o, lds_ld16(stg + (kf & 63)));
+            st16(o + 16, lds_ld16(stg + (kf & 63) + 16));
+            kf += 32;
+        }
+        // request the next 64 bytes ahead
+        if (live && !pfv && wb + kPW < iend) {
+            load64(s, wb + kPW, iend, pf);
+            pfv = true;
+        }
+        // ---- the common sequence, straight-line, until too few lanes can go on
+        RP_MARK(1);
+        const int32_t thr = min(LZ4M_PARSE_MIN_ACTIVE, (int)__popcll(__ballot(live)));
+        while (true) {
+            const bool go = live && !need;
+            if ((int)__popcll(__ballot(go)) < max(thr, 1)) break;
+            RP_COUNT(3, 1);
+            RP_COUNT(5, __popcll(__ballot(go)));
+            if (go) {
+                // straight-line: no short-circuit tests
+                const bool inw = ip + 16 <= wb + kPW;
+                const u32x4 w = lds_ld16(W + (ip & (kPW - 1)));
+                const int32_t tok = (int32_t)(w.x & 0xFFu), lit = tok >> 4, mlc = tok & 15;
+                const bool mlx = mlc == 15;
+                const uint32_t dw = dword_at(w, (uint32_t)(1 + lit));   // offset, then the match-length byte
+                const int32_t off = (int32_t)(dw & 0xFFFFu);
+                const int32_t ext = (int32_t)((dw >> 16) & 0xFFu);
+                const int32_t adv = 3 + lit + (int32_t)mlx;
+                const int32_t ml = mlc + 4 + (mlx ? ext : 0);
+                const bool ok = inw & (lit <= 12) & !(mlx & (ext == 255)) & (ip + 1 <= iend - 17) &
+                                (!mlx | (ip + adv <= iend - 4)) & (off != 0) & (off <= op + lit) &
+                                (op + lit + ml < oend - 64) & (k - kf < kPStage - 1);
+                // slot k is free (one slot of the ring always is): written even
+                // when the sequence is not taken, then overwritten
+                stg[k & (kPStage - 1)] = (uint8_t)adv;
+                ip += ok ? adv : 0;
+                op += ok ? lit + ml : 0;
+                k += (int32_t)ok;
+                need = !ok;
+            }
         }
     }
+    RP_FLUSH(0, 8);
 }
 
 // ------------------------------------------------------- 2. row execution
@@ -375,6 +476,124 @@ __device__ __forceinline__ uint32_t dword32(u32x4 a, u32x4 b, uint32_t k) {
     return __builtin_amdgcn_alignbyte(hi, lo, k & 3);
 }
 
+// Period-`off` pattern of the first off (1..15) bytes of w, E[j] = w[j % off]:
+// per output dword, v_perm from bytes 0-7 and from bytes 8-15 with
+// selectors from the table `sel` (8 dwords per offset; 0x0C selects zero).
+typedef __attribute__((address_space(3))) const uint32_t lds_cu32;
+__device__ __forceinline__ u32x4 period_perm(u32x4 w, lds_cu32* sel) {
+    u32x4 r;
+    r.x = __builtin_amdgcn_perm(w.y, w.x, sel[0]) | __builtin_amdgcn_perm(w.w, w.z, sel[1]);
+    r.y = __builtin_amdgcn_perm(w.y, w.x, sel[2]) | __builtin_amdgcn_perm(w.w, w.z, sel[3]);
+    r.z = __builtin_amdgcn_perm(w.y, w.x, sel[4]) | __builtin_amdgcn_perm(w.w, w.z, sel[5]);
+    r.w = __builtin_amdgcn_perm(w.y, w.x, sel[6]) | __builtin_amdgcn_perm(w.w, w.z, sel[7]);
+    return r;
+}
+
+// One round of a row, parsed: lane jj's sequence (start t, literal at t + lp,
+// lit / off / ml), its output position o, the round's row totals, the
+// literal's first 32 bytes and the far sources requested from HBM.
+struct PSeq {
+    u32x4 x0, x1, pre0, pre1;
+    int32_t t, lp, lit, off, ml, o, dlt;
+    int32_t use, opn, ipn;   // uniform across the row
+    uint32_t fl;
+};
+constexpr uint32_t kFlU = 1, kFlFar = 2, kFlLate = 4, kFlLitHbm = 8;
+
+// Parse the row's round at (k0, ip, op): lane jj's length byte dlt, its
+// start t and its 32 input bytes wa|wb (wb is clamped into the block, so
+// bytes >= 16 are valid only if t + 32 <= iend).  bnext is the history base
+// the round will run with; sources below it are requested now if they lie
+// below F (flushed), else marked late (requested once flushed).
+__device__ __forceinline__ void parse_round(PSeq& P, int32_t jj, int32_t r, int32_t k0, int32_t nseq, int32_t ip,
+                                            int32_t op, int32_t bnext, int32_t F, const uint8_t* s, const uint8_t* d,
+                                            int32_t iend, int32_t dlt, int32_t t, u32x4 wa, u32x4 wb) {
+    const bool act = k0 + jj < nseq;
+    const bool esc = dlt == 255;   // length >= 255: the parse left it to be re-parsed
+    const bool wbok = t + 32 <= iend;
+    const uint32_t tok = wa.x & 0xFFu;
+    const int32_t lit0 = (int32_t)(tok >> 4);
+    const bool litx = lit0 == 15;
+    const int32_t lit = lit0 + (litx ? (int32_t)byte_of(wa, 1) : 0);   // one extra byte unless escaped
+    const int32_t lp = litx ? 2 : 1;
+    const int32_t po = lp + lit;
+    const int32_t mlc = (int32_t)(tok & 15u);
+    // offset and first match-length byte: from wa for lit <= 12, else from wa|wb
+    const uint32_t pq = (uint32_t)(po < 28 ? po : 28);
+    const uint32_t dwo = lit <= 12 ? window_dword(wa, (uint32_t)po) : dword32(wa, wb, pq);
+    const uint32_t bsh = 8u * ((uint32_t)po - pq);
+    int32_t off = (int32_t)((dwo >> bsh) & 0xFFFFu);
+    const int32_t e0 = (int32_t)((dwo >> (bsh + 16)) & 0xFFu);
+    int32_t ml = mlc + (mlc == 15 ? e0 : 0);
+    const bool slow = (po + 3 > 32) | ((mlc == 15) & (e0 == 255)) | ((po + 3 > 16) & !wbok);
+    if (slow && act && !esc) {   // a long match length, or the offset past the bytes at hand: from HBM
+        const uint8_t* q = s + t;
+        off = (int32_t)q[po] | ((int32_t)q[po + 1] << 8);
+        ml = mlc;
+        if (ml == 15) {
+            int32_t pe = po + 2;
+            uint32_t b;
+            do {
+                b = q[pe];
+                ++pe;
+                ml += (int32_t)b;
+            } while (b == 255 && pe < iend - t);
+        }
+    }
+    ml += 4;
+    const int32_t len = act && !esc ? lit + ml : 0;
+    const int32_t o = op + row_incl_sum(len) - len;
+    const int32_t mend = o + lit + ml;
+    const bool ok = act & !esc & (mend <= bnext + kRowsH);
+    const uint32_t rb = (uint32_t)(__ballot(!ok) >> (16 * r)) & 0xFFFFu;
+    const int32_t use = rb ? __builtin_ctz(rb) : 16;
+    const bool u = jj < use;
+    P.opn = op + row_last(row_incl_sum(u ? len : 0));
+    P.ipn = ip + row_last(row_incl_sum(u ? dlt : 0));
+    P.use = use;
+    const int32_t s0 = o + lit - off;
+    const bool far = u & (s0 < bnext);
+    const bool late = far & (s0 + 32 > F);
+    const bool pf = far & !late;
+    // unconditional requests (lanes without a far source read the block start)
+    P.pre0 = ld16(d + (pf ? s0 : 0));
+    P.pre1 = ld16(d + (pf ? s0 + 16 : 0));
+    const uint32_t sh = (uint32_t)lp;
+    P.x0 = u32x4{__builtin_amdgcn_alignbyte(wa.y, wa.x, sh), __builtin_amdgcn_alignbyte(wa.z, wa.y, sh),
+                 __builtin_amdgcn_alignbyte(wa.w, wa.z, sh), __builtin_amdgcn_alignbyte(wb.x, wa.w, sh)};
+    P.x1 = u32x4{__builtin_amdgcn_alignbyte(wb.y, wb.x, sh), __builtin_amdgcn_alignbyte(wb.z, wb.y, sh),
+                 __builtin_amdgcn_alignbyte(wb.w, wb.z, sh), __builtin_amdgcn_alignbyte(0u, wb.w, sh)};
+    P.t = t;
+    P.lp = lp;
+    P.lit = lit;
+    P.off = off;
+    P.ml = ml;
+    P.o = o;
+    P.dlt = dlt;
+    P.fl = (u ? kFlU : 0u) | (far ? kFlFar : 0u) | (late ? kFlLate : 0u) |
+           ((u & (lp + lit > 16) & ((lp + lit > 32) | !wbok)) ? kFlLitHbm : 0u);
+}
+
+// history base a row runs its next round with, given the output position op
+__device__ __forceinline__ int32_t next_base(int32_t op, int32_t base) {
+    return op - base > kRowsH - kRowsRoom ? ((op - kRowsKeep) & ~15) : base;
+}
+
+// the round's inputs: 32 bytes at t (clamped into the block) and a length byte
+__device__ __forceinline__ void load_in(const uint8_t* s, int32_t t, int32_t iend, u32x4& a, u32x4& b) {
+    const int32_t ta = t + 16 <= iend ? t : 0;   // good sequences: t + 16 < iend
+    const int32_t tb = t + 32 <= iend ? t + 16 : iend - 16;
+    a = ld16(s + ta);
+    b = ld16(s + tb);
+}
+__device__ __forceinline__ int32_t load_len(const uint8_t* dl, int32_t k, int32_t nseq) {
+    const int32_t v = (int32_t)dl[k < nseq ? k : nseq - 1];
+    return k < nseq ? v : 0;
+}
+
+// Rows in flight: round R executes while round R + 1 is already parsed
+// (its far sources in flight) and round R + 2's inputs are requested, so a
+// round waits on no memory latency of its own.
 __global__ __launch_bounds__(64) void rows_exec_kernel(const uint8_t* __restrict__ src,
                                                        const int64_t* __restrict__ src_off,
                                                        const int32_t* __restrict__ src_len, uint8_t* dst,
@@ -383,20 +602,37 @@ __global__ __launch_bounds__(64) void rows_exec_kernel(const uint8_t* __restrict
                                                        const uint8_t* __restrict__ lens, int64_t n,
                                                        unsigned long long* __restrict__ ctr) {
     __shared__ __attribute__((aligned(16))) uint8_t hists[4 * kRowsHS];
+    __shared__ __attribute__((aligned(16))) uint8_t dums[64 * 16];
+    __shared__ __attribute__((aligned(16))) uint32_t psel[16 * 8];
     const uint32_t lane = threadIdx.x;
     const int32_t jj = (int32_t)(lane & 15), r = (int32_t)(lane >> 4);
     lds_u8* HB = (lds_u8*)(hists + r * kRowsHS);
+    lds_u8* DUM = (lds_u8*)(dums + lane * 16);
+    // period selectors: entry (off, i) for output dword i>>1, bytes 0-7 (i even) or 8-15
+    for (int e = (int)lane; e < 16 * 8; e += 64) {
+        const uint32_t o = (uint32_t)e >> 3, i = (uint32_t)e & 7, hi = i & 1;
+        uint32_t v = 0;
+        for (uint32_t b = 0; b < 4; ++b) {
+            const uint32_t x = o ? (4 * (i >> 1) + b) % o : 0;
+            const uint32_t sb = hi ? (x >= 8 ? x - 8 : 0x0C) : (x < 8 ? x : 0x0C);
+            v |= sb << (8 * b);
+        }
+        psel[e] = v;
+    }
+    lds_cu32* PS = (lds_cu32*)psel;
     // row state (uniform across the row's 16 lanes)
     const uint8_t* s = nullptr;
     uint8_t* d = nullptr;
     const uint8_t* dl = nullptr;
     int32_t iend = 0, nseq = 0, k0 = 0, ip = 0, op = 0, base = 0, F = 0;
-    bool have = false, pf = false;
-    // this round's inputs (valid when pf): length dc, start tc, bytes wa|wb;
-    // dn = the next round's length
-    int32_t dc = 0, tc = 0, dn = 0;
-    u32x4 wa = u32x4{0, 0, 0, 0}, wb = wa;
+    bool have = false, sync = true;
+    PSeq P, Q;   // P: the round to execute; Q: the next one, parsed ahead
+    // inputs of the round after Q: start tn, bytes na|nb, length dn; dnn = the one after
+    int32_t tn = 0, dn = 0, dnn = 0;
+    u32x4 na = u32x4{0, 0, 0, 0}, nb = na;
+    RP_DECL
     while (true) {
+        RP_MARK(14);
         if (!have) {
             unsigned long long b = 0;
             if (jj == 0) b = atomicAdd(&ctr[2], 1ull);
@@ -413,74 +649,24 @@ __global__ __launch_bounds__(64) void rows_exec_kernel(const uint8_t* __restrict
             nseq = mt.nseq;
             k0 = ip = op = base = F = 0;
             have = true;
-            pf = false;
+            sync = true;
         }
-        // keep kRowsRoom bytes of room; never drop unflushed bytes (F >= op - 15)
-        if (op - base > kRowsH - kRowsRoom) {
-            const int32_t nb = (op - kRowsKeep) & ~15;
-            for (int32_t c = 16 * jj; c < op - nb; c += 256) lds_st16(HB + c, lds_ld16(HB + (nb - base) + c));
-            base = nb;
+        RP_MARK(8);
+        if (sync) {   // block start, or the last round stopped early: parse this round now
+            RP_COUNT(19, 1);
+            const int32_t dc = load_len(dl, k0 + jj, nseq);
+            const int32_t tc = ip + row_incl_sum(dc) - dc;
+            u32x4 wa, wb;
+            load_in(s, tc, iend, wa, wb);
+            parse_round(P, jj, r, k0, nseq, ip, op, base, F, s, d, iend, dc, tc, wa, wb);
+            dn = load_len(dl, k0 + 16 + jj, nseq);
+            tn = P.ipn + row_incl_sum(dn) - dn;
+            load_in(s, tn, iend, na, nb);
+            dnn = load_len(dl, k0 + 32 + jj, nseq);
+            sync = false;
         }
-        // ---- the round: lane jj takes sequence k0 + jj
-        const int32_t k = k0 + jj;
-        const bool act = k < nseq;
-        if (!pf) {   // block start, or the last round stopped early: load now
-            dc = act ? (int32_t)dl[k] : 0;
-            tc = ip + row_incl_sum(dc) - dc;
-            load32(s, tc, iend, act, wa, wb);
-            dn = k + 16 < nseq ? (int32_t)dl[k + 16] : 0;
-        }
-        const int32_t t = tc, dlt = dc;
-        const bool esc = dlt == 255;   // length >= 255: the parse left it to be re-parsed
-        const uint32_t tok = wa.x & 0xFFu;
-        int32_t lit = (int32_t)(tok >> 4), lp = 1;
-        if (lit == 15) {
-            lit += (int32_t)byte_of(wa, 1);   // one extra byte unless the length escaped
-            lp = 2;
-        }
-        const int32_t po = lp + lit;
-        int32_t off = 0, ml = (int32_t)(tok & 15u);
-        bool slow = false;
-        if (lit <= 12) {
-            off = (int32_t)(window_dword(wa, (uint32_t)po) & 0xFFFFu);
-            if (ml == 15) {
-                const int32_t e = (int32_t)byte_of(wa, po + 2);
-                ml += e;
-                slow = e == 255;
-            }
-        } else if (po + 3 <= 32) {
-            off = (int32_t)(dword32(wa, wb, (uint32_t)po) & 0xFFFFu);
-            if (ml == 15) {
-                const int32_t e = (int32_t)((dword32(wa, wb, (uint32_t)(po + 2 < 28 ? po + 2 : 28)) >> (8 * (po + 2 - (po + 2 < 28 ? po + 2 : 28)))) & 0xFFu);
-                ml += e;
-                slow = e == 255;
-            }
-        } else {
-            slow = true;
-        }
-        if (slow && act && !esc) {   // a long match length or the offset past 32 bytes: from HBM
-            const uint8_t* q = s + t;
-            off = (int32_t)q[po] | ((int32_t)q[po + 1] << 8);
-            ml = (int32_t)(tok & 15u);
-            if (ml == 15) {
-                int32_t pe = po + 2;
-                uint32_t b;
-                do {
-                    b = q[pe];
-                    ++pe;
-                    ml += (int32_t)b;
-                } while (b == 255 && pe < iend - t);
-            }
-        }
-        ml += 4;
-        const int32_t len = act && !esc ? lit + ml : 0;
-        const int32_t o = op + row_incl_sum(len) - len;
-        const int32_t m = o + lit, mend = m + ml;
-        const bool ok = act && !esc && mend <= base + kRowsH;
-        const uint32_t rb = (uint32_t)(__ballot(!ok) >> (16 * r)) & 0xFFFFu;
-        const int32_t use = rb ? __builtin_ctz(rb) : 16;
-        if (use == 0) {
-            pf = false;
+        if (P.use == 0) {
+            sync = true;
             if (k0 >= nseq) {   // the block's good prefix is done: flush the rest exactly
                 for (int32_t c = F + 16 * jj; c < op; c += 256) gbl_put(d + c, lds_ld16(HB + (c - base)), op - c);
                 have = false;
@@ -525,87 +711,123 @@ __global__ __launch_bounds__(64) void rows_exec_kernel(const uint8_t* __restrict
             F = op;
             continue;
         }
-        const bool u = jj < use;
-        const int32_t opn = op + row_last(row_incl_sum(u ? len : 0));
-        const int32_t ipn = ip + row_last(row_incl_sum(u ? dlt : 0));
-        // the next round's lengths and bytes, requested now (valid if this
-        // round takes all 16 sequences)
-        const bool pfn = use == 16;
-        int32_t tn = 0, dn2 = 0;
-        u32x4 na = u32x4{0, 0, 0, 0}, nb2 = na;
-        if (pfn) {
-            const int32_t kn = k0 + 16 + jj;
-            tn = ipn + row_incl_sum(dn) - dn;
-            load32(s, tn, iend, kn < nseq, na, nb2);
-            dn2 = kn + 16 < nseq ? (int32_t)dl[kn + 16] : 0;
+        RP_MARK(10);
+        RP_COUNT(16, 1);
+        RP_COUNT(18, __popcll(__ballot((P.fl & kFlU) != 0)));
+        // ---- parse the next round ahead (its far sources are requested now),
+        // then request the inputs of the round after it
+        const bool ahead = P.use == 16 && k0 + 16 < nseq;
+        if (ahead) {
+            const int32_t bq = next_base(P.opn, base);
+            parse_round(Q, jj, r, k0 + 16, nseq, P.ipn, P.opn, bq, F, s, d, iend, dn, tn, na, nb);
+            dn = dnn;
+            tn = Q.ipn + row_incl_sum(dn) - dn;
+            load_in(s, tn, iend, na, nb);
+            dnn = load_len(dl, k0 + 48 + jj, nseq);
         }
-        const int32_t s0 = m - off;
-        // sources older than the buffer: their first 32 bytes are requested now
-        const bool far = u && s0 < base;
-        u32x4 pre0 = u32x4{0, 0, 0, 0}, pre1 = pre0;
-        if (far) {
-            pre0 = ld16(d + s0);
-            if (ml > 16) pre1 = ld16(d + s0 + 16);
-        }
-        if (u && lit > 0) {
-            if (lit <= 12) {
-                lds_put(HB + (o - base), window_shift1(wa), lit);
-            } else if (lp + lit <= 32) {
-                const uint32_t sh = (uint32_t)lp;
-                const u32x4 x0 = u32x4{__builtin_amdgcn_alignbyte(wa.y, wa.x, sh), __builtin_amdgcn_alignbyte(wa.z, wa.y, sh),
-                                       __builtin_amdgcn_alignbyte(wa.w, wa.z, sh), __builtin_amdgcn_alignbyte(wb.x, wa.w, sh)};
-                const u32x4 x1 = u32x4{__builtin_amdgcn_alignbyte(wb.y, wb.x, sh), __builtin_amdgcn_alignbyte(wb.z, wb.y, sh),
-                                       __builtin_amdgcn_alignbyte(wb.w, wb.z, sh), __builtin_amdgcn_alignbyte(0u, wb.w, sh)};
-                lds_put(HB + (o - base), x0, lit);
-                if (lit > 16) lds_put(HB + (o - base + 16), x1, lit - 16);
-            } else {   // a literal beyond the 32 bytes: from HBM (inside the block: good)
-                for (int32_t i = 0; i < lit; i += 16) lds_put(HB + (o - base + i), ld16(s + t + lp + i), lit - i);
+        RP_MARK(11);
+        // ---- execute round P
+        const bool u = (P.fl & kFlU) != 0;
+        const int32_t lit = P.lit, off = P.off, ml = P.ml, o = P.o;
+        const int32_t m = o + lit, mend = m + ml, s0 = m - off;
+        // literals: bytes lp.. of the input (exact, branch-free); longer ones rare
+        lds_put_bf(HB + (o - base), DUM, P.x0, u ? lit : 0);
+        if (u && lit > 16) {
+            if (!(P.fl & kFlLitHbm)) {
+                lds_put(HB + (o - base + 16), P.x1, lit - 16);
+            } else {   // a literal beyond the bytes at hand: from HBM (inside the block: good)
+                for (int32_t i = 16; i < lit; i += 16) lds_put(HB + (o - base + i), ld16(s + P.t + P.lp + i), lit - i);
             }
         }
+        RP_MARK(12);
         // readiness passes: a match is copied once no earlier pending match of
         // the round writes into its source [s0, se)
+        const bool far = (P.fl & kFlFar) != 0, late = (P.fl & kFlLate) != 0;
+        u32x4 g0 = P.pre0;
+        if (__any(late)) {   // a source flushed only by the previous round (rare): load it now
+            const u32x4 lv = ld16(d + (late ? s0 : 0));
+            g0 = late ? lv : g0;
+        }
         const int32_t se = s0 + (off < ml ? off : ml);
+        const bool per = off < 16;   // period pattern (s0 >= base here: m - base >= off)
+        const int32_t stp = per ? 16 - (16 % off) : 16;
         bool pend = u;
         while (__any(pend)) {
-            const int32_t x = row_excl_max(pend ? mend : -1);
-            const int32_t y = row_excl_min(pend ? m : INT_MAX);
-            const bool ready = pend && (x <= s0 || se <= y);
-            if (ready) {
-                if (off >= 16) {
-                    for (int32_t i = 0; i < ml; i += 16) {
+            RP_COUNT(17, 1);
+            // x1 = 1 + the end of the nearest pending match below, y1 = BIG -
+            // the start of the first pending match below (0: none)
+            int32_t x1, y1;
+            row_excl_max2(pend ? mend + 1 : 0, pend ? 0x3FFFFFFF - m : 0, x1, y1);
+            const bool ready = pend & ((x1 <= s0 + 1) | (y1 <= 0x3FFFFFFF - se));
+            // first 16 bytes: branch-free
+            const u32x4 l0 = lds_ld16(HB + (s0 >= base ? s0 - base : 0));
+            u32x4 v0 = far ? g0 : l0;
+            if (__any(ready && per)) {
+                const u32x4 pp = period_perm(l0, PS + 8 * (per ? off : 0));
+                v0 = per ? pp : v0;
+            }
+            lds_put_bf(HB + (m - base), DUM, v0, ready ? ml : 0);
+            // the rest (matches longer than one step)
+            if (ready && ml > stp) {
+                for (int32_t i = stp; i < ml; i += stp) {
+                    u32x4 v;
+                    if (per) {
+                        v = v0;
+                    } else {
                         const int32_t sp = s0 + i;
                         // sp < base: flushed (F >= base + kRowsKeep - 16)
-                        const u32x4 v = (far && i < 32) ? (i == 0 ? pre0 : pre1)
-                                                        : sp >= base ? lds_ld16(HB + (sp - base)) : ld16(d + sp);
-                        lds_put(HB + (m - base + i), v, ml - i);
+                        v = (far && !late && i == 16) ? P.pre1 : sp >= base ? lds_ld16(HB + (sp - base)) : ld16(d + sp);
                     }
-                } else {   // s0 >= base: m - base >= off here
-                    const u32x4 pat = period_pattern(lds_ld16(HB + (s0 - base)), (uint32_t)off);
-                    const int32_t step = 16 - (16 % off);
-                    for (int32_t i = 0; i < ml; i += step) lds_put(HB + (m - base + i), pat, ml - i);
+                    lds_put(HB + (m - base + i), v, ml - i);
                 }
             }
             pend = pend && !ready;
         }
-        if (pfn) {
-            dc = dn;
-            tc = tn;
-            wa = na;
-            wb = nb2;
-            dn = dn2;
-        }
-        pf = pfn;
+        RP_MARK(13);
+        // ---- flush, advance, rebase for the next round
+        const int32_t opn = P.opn;
         for (int32_t c = F + 16 * jj; c + 16 <= opn; c += 256) st16(d + c, lds_ld16(HB + (c - base)));
         F += (opn - F) & ~15;
         op = opn;
-        ip = ipn;
-        k0 += use;
+        ip = P.ipn;
+        k0 += P.use;
+        const int32_t nbse = next_base(op, base);
+        if (nbse != base) {
+            // the kept bytes lie >= kRowsH - kRowsRoom - kRowsKeep past the
+            // buffer start: all reads of a group before its writes
+            for (int32_t c0 = 0; c0 < op - nbse; c0 += 1024) {
+                u32x4 v[4];
+#pragma unroll
+                for (int g = 0; g < 4; ++g) v[g] = lds_ld16(HB + (nbse - base) + c0 + 256 * g + 16 * jj);
+#pragma unroll
+                for (int g = 0; g < 4; ++g) lds_st16(HB + c0 + 256 * g + 16 * jj, v[g]);
+            }
+            base = nbse;
+        }
+        if (ahead) {
+            P = Q;
+        } else {
+            sync = true;
+        }
+        RP_MARK(9);
     }
+    RP_FLUSH(8, 24);
 }
 
 }  // namespace lz4m
 
 using namespace lz4m;
+
+#ifdef LZ4M_ROWS_PROF
+extern "C" int lz4m_rows_prof(unsigned long long* out, int reset) {
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(lz4m::g_rows_prof), sizeof(unsigned long long) * 32);
+    if (e == hipSuccess && reset) {
+        unsigned long long z[32] = {0};
+        e = hipMemcpyToSymbol(HIP_SYMBOL(lz4m::g_rows_prof), z, sizeof(z));
+    }
+    return (int)e;
+}
+#endif
 
 extern "C" size_t lz4m_rows_fixed_bytes(int64_t n) { return 64 + (size_t)n * sizeof(RowMeta); }
 
