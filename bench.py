@@ -13,15 +13,22 @@ LZ4_compress_default (tests/test_gpu_codec.py) -- i.e. the decompress input
 is exactly what lz4libs would produce.  Output is verified bit-exact against
 the original blocks at full size.
 
-Multi-GPU (torchrun, one process per GPU): every rank decodes its own
-1 M-block shard (weak scaling, no data-path collective); timing is the max
-over ranks between barriers.  value = all ranks' bytes / that time.
+Multi-GPU (one process per GPU; `--gpus N` without a launcher starts
+torch.distributed.run itself): every rank decodes its own 1 M-block shard
+(weak scaling, no data-path collective); timing is the max over ranks between
+barriers.  value = all ranks' bytes / that time.  Config 5 (compress a shard
+larger than HBM in waves, gather every wave's compressed output at rank 0
+over RCCL, the gather of wave k overlapped with the compression of wave k+1)
+is reported beside it, weak and strong scaling.
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -104,6 +111,18 @@ def time_kernel(fn, steps: int, warmup: int, world: int):
     return wall, ev_ms / 1e3
 
 
+def host_threads() -> int:
+    """Host threads for the CPU baselines: this process's CPU share.  The GPU
+    box gives one GPU's job 16 cores (OMP_NUM_THREADS) while nproc shows the
+    whole machine, so the share is min(affinity, OMP_NUM_THREADS or 16)."""
+    try:
+        vis = len(os.sched_getaffinity(0))
+    except AttributeError:
+        vis = os.cpu_count() or 1
+    share = int(os.environ.get("OMP_NUM_THREADS", "16") or 16)
+    return max(1, min(vis, share))
+
+
 def cpu_baseline(host_blocks: np.ndarray, comp_host: list, seconds: float = 10.0) -> dict:
     """Reference lz4libs (oracle/_ref, compiled from /root/reference) on the
     host cores: LZ4_decompress_safe over a bounded sample of the same
@@ -111,11 +130,7 @@ def cpu_baseline(host_blocks: np.ndarray, comp_host: list, seconds: float = 10.0
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O   # test/bench infrastructure only
     cb = O.CpuBench()
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cores = os.cpu_count() or 1
-    cores = max(1, min(cores, 16))   # the GPU box's CPU share is 16 cores
+    cores = host_threads()
     n = len(comp_host)
     lens = np.array([len(c) for c in comp_host], dtype=np.int32)
     src = np.frombuffer(b"".join(comp_host), dtype=np.uint8)
@@ -130,6 +145,7 @@ def cpu_baseline(host_blocks: np.ndarray, comp_host: list, seconds: float = 10.0
     assert np.array_equal(dst.reshape(n, BLOCK), host_blocks[:n]), "CPU baseline output mismatch"
     val = n * reps * BLOCK / secs / GIB
     res = {"value": round(val, 3), "unit": "GiB/s", "cores": cores, "kind": cb.kind,
+           "cores_note": "this process's CPU share (min of its affinity and OMP_NUM_THREADS, 16 on the GPU box)",
            "sample": f"LZ4_decompress_safe, {n} x 64 KiB silesia-like blocks x {reps} reps "
                      f"({secs:.1f} s, {cores} pthreads, one contiguous slice each)"}
     # the same decode on one core (all cores and 1 core), ~3 s
@@ -155,6 +171,138 @@ def cpu_baseline(host_blocks: np.ndarray, comp_host: list, seconds: float = 10.0
     return res
 
 
+def config5(src, n, world, rank, dev, wave_blocks, waves, total_blocks):
+    """BASELINE config 5: a shard larger than HBM is
+    compressed in waves over a resident working set (here: the rank's 1 M
+    generated blocks, a different window of them each wave), each wave
+    compacted and gathered at rank 0 over RCCL (lz4._dist), the gather of
+    wave k overlapped with the compression of wave k+1.  Weak scaling:
+    `waves` waves per rank; strong scaling: `total_blocks` over all ranks.
+    Parallel-parse compressor (config 3's kernel)."""
+    from lz4._dist import compress_gather_waves
+    bw = min(wave_blocks, n)
+    cap = N.compress_bound(BLOCK)
+    cap16 = (cap + 15) // 16 * 16
+    base_off = torch.arange(bw, dtype=torch.int64, device=dev) * BLOCK
+    src_len = torch.full((bw,), BLOCK, dtype=torch.int32, device=dev)
+    slots = torch.empty(bw * cap16, dtype=torch.uint8, device=dev)
+    slot_off = torch.arange(bw, dtype=torch.int64, device=dev) * cap16
+    slot_cap = torch.full((bw,), cap, dtype=torch.int32, device=dev)
+    out_len = torch.empty(bw, dtype=torch.int32, device=dev)
+    comp = [torch.empty(bw * cap16, dtype=torch.uint8, device=dev) for _ in range(2)]
+    windows = max(1, n // bw)
+
+    def compress_wave(w):
+        so = base_off + ((w % windows) * bw) * BLOCK
+        N.launch_compress(src, so, src_len, slots, slot_off, slot_cap, out_len, bw, N.PARSE_PARALLEL, 1)
+        offs = N.exclusive_scan(out_len)
+        buf = comp[w & 1]
+        N.gather(slots, slot_off, out_len, buf, offs, bw)
+        total = int(offs[bw])   # the wave's compacted size (host needs it to post the transfers)
+        return buf[:total], out_len
+
+    def run(nw):
+        box = {}
+        if world == 1:   # no exchange: compress + compact only
+            def go():
+                cb = 0
+                for w in range(nw):
+                    c, _ = compress_wave(w)
+                    cb += c.numel()
+                box["st"] = {"comp_bytes": cb, "gathered_bytes": 0}
+        else:
+            def go():
+                box["st"] = compress_gather_waves(compress_wave, nw, root=0)
+        wall, _ = time_kernel(go, 1, 1, world)
+        st = box["st"]
+        res = {"waves_per_rank": nw, "blocks_per_rank": nw * bw, "seconds": round(wall, 4),
+               "aggregate_gib_s": round(world * nw * bw * BLOCK / wall / GIB, 2),
+               "ratio": round(nw * bw * BLOCK / max(st["comp_bytes"], 1), 4)}
+        if world > 1:
+            g = torch.tensor([st["gathered_bytes"]], dtype=torch.int64, device=dev)
+            torch.distributed.all_reduce(g)
+            res["root_ingress_gb_s"] = round(int(g) / wall / 1e9, 2)
+        return res
+
+    out = {"wave_blocks_per_rank": bw, "block_size": BLOCK, "parse": "parallel (LZ4M_PARSE_PARALLEL)",
+           "gather": "rank 0 over RCCL, overlapped with the next wave" if world > 1 else "none (1 rank)",
+           "weak": run(waves)}
+    out["strong"] = dict(run(max(1, total_blocks // (world * bw))), total_blocks=total_blocks)
+    # the same waves without the exchange, for the compress-only rate per rank
+    if world > 1:
+        t0 = time.perf_counter()
+        for w in range(waves):
+            compress_wave(w)
+        torch.cuda.synchronize()
+        out["compress_only_gib_s_per_rank"] = round(waves * bw * BLOCK / (time.perf_counter() - t0) / GIB, 2)
+    del slots, comp
+    return out
+
+
+def config1(n_blocks: int, dev) -> dict:
+    """BASELINE config 1: the lz4.block.compress / decompress round trip on
+    n x 64 KiB random blocks (random.Random(12345)), through
+    the per-call drop-in API and through the batched host API, beside the
+    reference lz4libs (oracle/_ref) on 1 host thread and on all of them."""
+    import random
+    import lz4.block as LB
+    rnd = random.Random(12345)
+    blocks = [rnd.randbytes(BLOCK) for _ in range(n_blocks)]
+    tot = n_blocks * BLOCK
+    LB.decompress(LB.compress(blocks[0]))   # warm the staging buffers
+    t0 = time.perf_counter()
+    comp = [LB.compress(b) for b in blocks]
+    t1 = time.perf_counter()
+    back = [LB.decompress(c) for c in comp]
+    t2 = time.perf_counter()
+    assert back == blocks, "config 1 round trip failed"
+    t3 = time.perf_counter()
+    cm = LB.compress_many(blocks)
+    t4 = time.perf_counter()
+    bm = LB.decompress_many(cm)
+    t5 = time.perf_counter()
+    assert bm == blocks and cm == comp, "config 1 batched round trip failed"
+    res = {"blocks": n_blocks, "data": "random.Random(12345).randbytes(65536) per block",
+           "per_call_compress_us": round((t1 - t0) / n_blocks * 1e6, 1),
+           "per_call_decompress_us": round((t2 - t1) / n_blocks * 1e6, 1),
+           "per_call_roundtrip_gib_s": round(tot / (t2 - t0) / GIB, 3),
+           "batched_compress_gib_s": round(tot / (t4 - t3) / GIB, 3),
+           "batched_decompress_gib_s": round(tot / (t5 - t4) / GIB, 3),
+           "batched_roundtrip_gib_s": round(tot / (t5 - t3) / GIB, 3)}
+    # reference lz4libs on the host cores (LZ4_compress_default is byte-identical
+    # to lz4.block.compress on random data, SURVEY 0.1)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O   # test/bench infrastructure only
+    cb = O.CpuBench()
+    raw = np.frombuffer(b"".join(blocks), dtype=np.uint8)
+    r_off = np.arange(n_blocks, dtype=np.int64) * BLOCK
+    r_len = np.full(n_blocks, BLOCK, dtype=np.int32)
+    cstride = 65824
+    cdst = np.empty(n_blocks * cstride, dtype=np.uint8)
+    c_off = np.arange(n_blocks, dtype=np.int64) * cstride
+    c_cap = np.full(n_blocks, cstride, dtype=np.int32)
+    dst = np.empty(n_blocks * BLOCK, dtype=np.uint8)
+    cores = host_threads()
+    for th in sorted({1, cores}):
+        sc, outc = cb.run("compress", th, 3, raw, r_off, r_len, cdst, c_off, c_cap)
+        sd, outd = cb.run("decompress", th, 3, cdst, c_off, outc.astype(np.int32), dst, r_off, r_len)
+        assert (outd == BLOCK).all()
+        key = "ref_1thread" if th == 1 else f"ref_{th}threads"
+        res[key] = {"compress_gib_s": round(3 * tot / sc / GIB, 3), "decompress_gib_s": round(3 * tot / sd / GIB, 3),
+                    "roundtrip_gib_s": round(3 * tot / (sc + sd) / GIB, 3), "kind": cb.kind}
+    return res
+
+
+def decoder_src_sha() -> str:
+    """Identity of the decoder kernels that profiles/pmc_decompress.json
+    must have been measured on (roofline.traffic is reported only on a match)."""
+    h = hashlib.sha256()
+    for f in ("lz4m_rows.hip", "lz4m_rows.h", "lz4m_decompress.hip", "lz4m_common.h"):
+        with open(os.path.join(ROOT, "python-lz4_amd", "csrc", f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -165,15 +313,33 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-compress", action="store_true")
     ap.add_argument("--random-blocks", type=int, default=1 << 17, help="blocks of the random-data extra line")
-    ap.add_argument("--gather-blocks", type=int, default=1 << 16,
-                    help="N>1: compressed blocks per rank gathered at rank 0 over RCCL (config 5 exchange)")
     ap.add_argument("--frame-gib", type=int, default=8,
                     help="config 4: GiB of input in one LZ4 frame of 4 MiB independent blocks + content checksum; 0 = skip")
     ap.add_argument("--e2e-blocks", type=int, default=1 << 18,
                     help="blocks of the host-to-host (PCIe-inclusive) extra line; 0 = skip")
+    ap.add_argument("--c5-wave-blocks", type=int, default=1 << 16,
+                    help="config 5: 64 KiB blocks per rank per wave (compressed, compacted, gathered at rank 0)")
+    ap.add_argument("--c5-waves", type=int, default=4, help="config 5 weak scaling: waves per rank")
+    ap.add_argument("--c5-total", type=int, default=1 << 19,
+                    help="config 5 strong scaling: blocks in total over all ranks; 0 = skip config 5")
+    ap.add_argument("--c1-blocks", type=int, default=1000,
+                    help="config 1: random 64 KiB blocks through the per-call lz4.block API; 0 = skip")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        # one process per GPU: start the launcher as a child (nothing has
+        # touched the GPU in this process) and exit with its status
+        s0 = socket.socket()
+        s0.bind(("127.0.0.1", 0))
+        port = s0.getsockname()[1]
+        s0.close()
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+               "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+        raise SystemExit(subprocess.call(cmd))
+    world = int(world_env or "1")
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch one process per GPU")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
@@ -275,27 +441,10 @@ def main():
                                      "kernel_ms": round(m_ev * 1e3, 3),
                                      "kernel": "hist_decompress_kernel (one wave per block, output in LDS)"}
 
-    # ---- extra (N > 1): gather compressed shards at rank 0 over RCCL ----
-    if world > 1 and args.gather_blocks > 0:
-        from lz4._dist import gather_compressed
-        ng = min(args.gather_blocks, n)
-        g_bytes = int(c_off[ng - 1]) + int(c_len[ng - 1])
-        g_comp, g_len = comp[:g_bytes], c_len[:ng]
-        box = {}
-
-        def do_gather():
-            box["r"] = gather_compressed(g_comp, g_len, root=0)
-
-        g_wall, _ = time_kernel(do_gather, 1, 1, world)
-        tot = torch.tensor([g_bytes], dtype=torch.int64, device=dev)
-        torch.distributed.all_reduce(tot)
-        if rank == 0:
-            buf, _, lens = box["r"]
-            assert buf.numel() == int(tot) and lens.numel() == world * ng
-            assert torch.equal(buf[:g_bytes], g_comp)
-        extra["gather_compressed_gb_s"] = round(int(tot) / g_wall / 1e9, 2)
-        extra["gather_blocks_per_rank"] = ng
-        box.clear()
+    # ---- config 5: compress in waves, gather every wave at rank 0 (RCCL) ----
+    if args.c5_total > 0:
+        extra["config5"] = config5(src, n, world, rank, dev, args.c5_wave_blocks, args.c5_waves, args.c5_total)
+        log("[bench] config 5 done")
 
     # ---- extra: end to end from pinned host memory (PCIe-inclusive) ----
     # lz4.block.decompress_host: chunks of 65 536 blocks pipelined over three
@@ -405,6 +554,11 @@ def main():
         del fsrc, frame, meta
         torch.cuda.empty_cache()
 
+    # ---- config 1: the per-call drop-in path (host bytes in, host bytes out) ----
+    if args.c1_blocks > 0 and world == 1 and not args.no_cpu:
+        extra["config1"] = config1(args.c1_blocks, dev)
+        log("[bench] config 1 done")
+
     # ---- report ----
     d_step = d_wall / args.steps
     value = world * n * BLOCK / d_step / GIB
@@ -419,7 +573,8 @@ def main():
         try:
             with open(pmc_path) as f:
                 pmc = json.load(f)
-            if pmc.get("blocks") == n and pmc.get("pool") == args.pool:
+            if (pmc.get("blocks") == n and pmc.get("pool") == args.pool
+                    and pmc.get("decoder_src_sha") == decoder_src_sha()):
                 traffic = pmc.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None

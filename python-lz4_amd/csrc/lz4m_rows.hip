@@ -557,7 +557,7 @@ __device__ __forceinline__ void parse_round(PSeq& P, int32_t jj, int32_t r, int3
     const bool pf = far & !late;
     // unconditional requests (lanes without a far source read the block start)
     P.pre0 = ld16(d + (pf ? s0 : 0));
-    P.pre1 = ld16(d + (pf ? s0 + 16 : 0));
+    P.pre1 = ld16(d + ((pf & (ml > 16)) ? s0 + 16 : 0));
     const uint32_t sh = (uint32_t)lp;
     P.x0 = u32x4{__builtin_amdgcn_alignbyte(wa.y, wa.x, sh), __builtin_amdgcn_alignbyte(wa.z, wa.y, sh),
                  __builtin_amdgcn_alignbyte(wa.w, wa.z, sh), __builtin_amdgcn_alignbyte(wb.x, wa.w, sh)};

@@ -131,16 +131,91 @@ def decompress(source, uncompressed_size=-1, return_bytearray=False, dict=None):
 
 
 # ---------------------------------------------------- host-buffer batches
-def _pack_host(views) -> tuple[bytearray, list[int], list[int]]:
-    offs, lens, total = [], [], 0
+# A call from host memory moves everything through one pinned staging buffer
+# per thread and device: block table + payload in ONE host-to-device copy,
+# status/lengths + output in ONE device-to-host copy (the reference does one
+# malloc + memcpy per call, _block.c:215, :256-263; a launch per small tensor
+# would dominate a 64 KiB call).
+import threading
+
+import numpy as np
+
+_tls = threading.local()
+_ALIGN = 256
+
+
+def _al(x: int) -> int:
+    return (x + _ALIGN - 1) // _ALIGN * _ALIGN
+
+
+def _stage(dev, host_bytes: int, dev_bytes: int):
+    """(pinned host uint8, device uint8) buffers of at least these sizes,
+    cached per thread and device, grown geometrically."""
+    cache = getattr(_tls, "stage", None)
+    if cache is None:
+        cache = _tls.stage = {}
+    h, d = cache.get(dev, (None, None))
+    if h is None or h.numel() < host_bytes:
+        h = torch.empty(max(host_bytes, 2 * (h.numel() if h is not None else 0), 1 << 20), dtype=torch.uint8,
+                        pin_memory=True)
+    if d is None or d.numel() < dev_bytes:
+        d = torch.empty(max(dev_bytes, 2 * (d.numel() if d is not None else 0), 1 << 20), dtype=torch.uint8,
+                        device=dev)
+    cache[dev] = (h, d)
+    return h, d
+
+
+class _Layout:
+    """Byte layout of one staged batch: n-entry tables, then payload, then
+    (device only) the n-entry result table and the output region."""
+
+    def __init__(self, n: int, payload: int, out_bytes: int):
+        self.src_off = 0
+        self.src_len = _al(8 * n)
+        self.dst_off = self.src_len + _al(4 * n)
+        self.dst_cap = self.dst_off + _al(8 * n)
+        self.payload = self.dst_cap + _al(4 * n)
+        self.h2d = self.payload + payload                  # bytes copied in
+        self.result = _al(self.h2d)
+        self.out = self.result + _al(4 * n)
+        self.total = self.out + max(out_bytes, 1)            # device bytes
+        self.d2h = self.total - self.result                  # bytes copied out
+
+
+def _stage_in(dev, views, offs, lens, d_off, caps, skip=None):
+    """Stage tables + packed payload, copy them to the device in one go;
+    returns (layout, host, device) with the device views ready to launch on."""
+    n = len(views)
+    payload = sum(lens)
+    lay = _Layout(n, payload, sum(caps))
+    h, d = _stage(dev, lay.total, lay.total)
+    hn = h.numpy()
+    hn[lay.src_off:lay.src_off + 8 * n].view(np.int64)[:] = offs if skip is None else np.add(offs, skip)
+    hn[lay.src_len:lay.src_len + 4 * n].view(np.int32)[:] = lens if skip is None else np.subtract(lens, skip)
+    hn[lay.dst_off:lay.dst_off + 8 * n].view(np.int64)[:] = d_off
+    hn[lay.dst_cap:lay.dst_cap + 4 * n].view(np.int32)[:] = caps
+    pos = lay.payload
     for v in views:
-        offs.append(total)
-        lens.append(v.nbytes)
-        total += v.nbytes
-    packed = bytearray(total)
-    for v, o in zip(views, offs):
-        packed[o:o + v.nbytes] = v
-    return packed, offs, lens
+        hn[pos:pos + v.nbytes] = np.frombuffer(v, dtype=np.uint8)
+        pos += v.nbytes
+    d[:lay.h2d].copy_(h[:lay.h2d], non_blocking=True)
+    return lay, h, d
+
+
+def _dev_views(lay: _Layout, d: torch.Tensor, n: int):
+    def sl(a, nb, dt):
+        return d[a:a + nb].view(dt)
+    return (sl(lay.payload, max(lay.h2d - lay.payload, 1), torch.uint8), sl(lay.src_off, 8 * n, torch.int64),
+            sl(lay.src_len, 4 * n, torch.int32), d[lay.out:lay.total], sl(lay.dst_off, 8 * n, torch.int64),
+            sl(lay.dst_cap, 4 * n, torch.int32), sl(lay.result, 4 * n, torch.int32))
+
+
+def _stage_out(lay: _Layout, h: torch.Tensor, d: torch.Tensor, n: int):
+    """One device-to-host copy of the result table + output region."""
+    h[lay.result:lay.total].copy_(d[lay.result:lay.total], non_blocking=True)
+    torch.cuda.current_stream(d.device).synchronize()
+    hn = h.numpy()
+    return hn[lay.result:lay.result + 4 * n].view(np.int32).tolist(), hn[lay.out:lay.total]
 
 
 def compress_many(blocks, accel: int = 1, store_size: bool = True, as_bytearray: bool = False,
@@ -150,29 +225,25 @@ def compress_many(blocks, accel: int = 1, store_size: bool = True, as_bytearray:
     input larger than LZ4_MAX_INPUT_SIZE)."""
     views = [_buffer(b) for b in blocks]
     dev = N.device()
-    packed, offs, lens = _pack_host(views)
     n = len(views)
+    if n == 0:
+        return []
+    lens = [v.nbytes for v in views]
+    offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.int64)]) if n > 1 else np.zeros(1, np.int64)
     caps = [max(N.compress_bound(L), 1) for L in lens]
-    d_off = [0] * n
-    acc = 0
-    for i, c in enumerate(caps):
-        d_off[i] = acc
-        acc += c
-    d_src = N.to_device(packed, dev)
-    d_dst = torch.empty(max(acc, 1), dtype=torch.uint8, device=dev)
-    src_off, src_len = _i64(offs, dev), _i32(lens, dev)
-    dst_off, dst_cap = _i64(d_off, dev), _i32(caps, dev)
-    out_len = torch.empty(n, dtype=torch.int32, device=dev)
+    d_off = np.concatenate([[0], np.cumsum(caps[:-1], dtype=np.int64)]) if n > 1 else np.zeros(1, np.int64)
+    lay, h, d = _stage_in(dev, views, offs, lens, d_off, caps)
+    d_src, src_off, src_len, d_dst, dst_off, dst_cap, out_len = _dev_views(lay, d, n)
     N.launch_compress(d_src, src_off, src_len, d_dst, dst_off, dst_cap, out_len, n, table, accel)
-    host = d_dst.cpu().numpy()
-    olen = out_len.cpu().tolist()
+    olen, host = _stage_out(lay, h, d, n)
     res = []
     for i in range(n):
         L = olen[i]
         if L <= 0:
             res.append(None)
             continue
-        body = host[d_off[i]:d_off[i] + L].tobytes()
+        o = int(d_off[i])
+        body = host[o:o + L].tobytes()
         if store_size:
             body = lens[i].to_bytes(4, "little") + body
         res.append(bytearray(body) if as_bytearray else body)
@@ -190,6 +261,8 @@ def decompress_many(blocks, uncompressed_size=-1, dict=None, as_bytearray: bool 
     """
     views = [_buffer(b) for b in blocks]
     n = len(views)
+    if n == 0:
+        return []
     sizes = list(uncompressed_size) if isinstance(uncompressed_size, (list, tuple)) else [uncompressed_size] * n
     caps, skip, errors = [], [], [None] * n
     for i, (v, us) in enumerate(zip(views, sizes)):
@@ -217,17 +290,11 @@ def decompress_many(blocks, uncompressed_size=-1, dict=None, as_bytearray: bool 
             caps.append(cap)
             skip.append(_HDR)
     dev = N.device()
-    packed, offs, lens = _pack_host(views)
-    d_src = N.to_device(packed, dev)
-    src_off = _i64([o + s for o, s in zip(offs, skip)], dev)
-    src_len = _i32([L - s for L, s in zip(lens, skip)], dev)
-    d_off, acc = [], 0
-    for c in caps:
-        d_off.append(acc)
-        acc += c
-    d_dst = torch.empty(max(acc, 1), dtype=torch.uint8, device=dev)
-    dst_off, dst_cap = _i64(d_off, dev), _i32(caps, dev)
-    status = torch.empty(n, dtype=torch.int32, device=dev)
+    lens = [v.nbytes for v in views]
+    offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.int64)]) if n > 1 else np.zeros(1, np.int64)
+    d_off = np.concatenate([[0], np.cumsum(caps[:-1], dtype=np.int64)]) if n > 1 else np.zeros(1, np.int64)
+    lay, h, d = _stage_in(dev, views, offs, lens, d_off, caps, skip=skip)
+    d_src, src_off, src_len, d_dst, dst_off, dst_cap, status = _dev_views(lay, d, n)
     if dict is not None and _buffer(dict).nbytes:
         dv = _buffer(dict)
         d_dict = N.to_device(dv, dev)
@@ -235,9 +302,9 @@ def decompress_many(blocks, uncompressed_size=-1, dict=None, as_bytearray: bool 
                             dict_buf=d_dict, dict_off=torch.zeros(n, dtype=torch.int64, device=dev),
                             dict_len=torch.full((n,), dv.nbytes, dtype=torch.int32, device=dev))
     else:
-        N.launch_decompress(d_src, src_off, src_len, d_dst, dst_off, dst_cap, status, n)
-    st = status.cpu().tolist()
-    host = d_dst.cpu().numpy() if acc else None
+        N.launch_decompress(d_src, src_off, src_len, d_dst, dst_off, dst_cap, status, n,
+                            src_bytes=int(sum(lens)))
+    st, host = _stage_out(lay, h, d, n)
     res = []
     for i in range(n):
         if errors[i] is not None:
@@ -256,7 +323,8 @@ def decompress_many(blocks, uncompressed_size=-1, dict=None, as_bytearray: bool 
                 raise err
             res.append(err)
             continue
-        body = host[d_off[i]:d_off[i] + r].tobytes() if r else b""
+        o = int(d_off[i])
+        body = host[o:o + r].tobytes() if r else b""
         res.append(bytearray(body) if as_bytearray else body)
     return res
 
@@ -340,8 +408,9 @@ def decompress_host(comp: torch.Tensor, comp_off: torch.Tensor, comp_len: torch.
     the copies to overlap); comp_off / out_off int64, comp_len / out_cap
     int32 host tensors, blocks in increasing position order in both.
     Returns the int32 status of every block (host), as LZ4_decompress_safe
-    would return it.  A chunk needs >= 64 K blocks to keep the decoder busy
-    (a 64 KiB block takes one lane ~34 ms)."""
+    would return it.  Chunks of 64 K blocks or more run the large-batch
+    (rows) decoder; smaller chunks the one-wave-per-block decoder, which
+    needs ~16 K blocks to fill the chip."""
     dev = device or N.device()
     n = comp_off.numel()
     status = torch.empty(n, dtype=torch.int32, device=dev)

@@ -1,24 +1,33 @@
 """Per-launch counters of the decoder dispatches in a tools/pmc_bench.sh run.
 
-Dispatch order in `bench.py --steps 1 --warmup 0 --no-compress`: the first
-stage_decompress dispatch is the silesia-like headline launch (config 2);
-the next two are the random-data launches (warmup + step), whose bytes are
-known (pure streaming: read ~= compressed size, write = decoded size) and
-serve as the calibration of the request counters."""
+One decoder launch = the row decoder's three kernels (parse, execution,
+finisher); the k-th dispatch of each kernel belongs to launch k.  Launch
+order in `bench.py --steps 1 --warmup 0 --no-compress`: launch 0 is the
+silesia-like headline launch (config 2); the next two are the random-data
+launches (warmup + step), whose bytes are known (pure streaming: read ~=
+compressed size, write = decoded size) and serve as the calibration of the
+request counters.  The summary carries the hash of the decoder sources
+(bench.decoder_src_sha) so bench.py reports roofline.traffic only for the
+kernels that were profiled."""
 import collections
 import csv
 import glob
 import json
 import sys
 
+import os
+
+KERNELS = ("rows_parse_kernel", "rows_exec_kernel", "decompress_kernel<false, true>")
 d = sys.argv[1]
-per = collections.defaultdict(dict)   # dispatch order -> counter -> value
+per = collections.defaultdict(dict)   # launch order -> counter -> value
 for f in sorted(glob.glob(f"{d}/p*/p*_counter_collection.csv")):
-    rows = [r for r in csv.DictReader(open(f)) if "stage_decompress" in r["Kernel_Name"]]
-    order = sorted({int(r["Dispatch_Id"]) for r in rows})
-    for r in rows:
-        k = order.index(int(r["Dispatch_Id"]))
-        per[k][r["Counter_Name"]] = per[k].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    rows = list(csv.DictReader(open(f)))
+    for kn in KERNELS:
+        kr = [r for r in rows if kn in r["Kernel_Name"]]
+        order = sorted({int(r["Dispatch_Id"]) for r in kr})
+        for r in kr:
+            k = order.index(int(r["Dispatch_Id"]))
+            per[k][r["Counter_Name"]] = per[k].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
 out = {k: v for k, v in sorted(per.items())}
 print(json.dumps(out, indent=1))
 
@@ -31,11 +40,13 @@ def hbm_bytes(c):
     return rd, wr
 
 
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 if len(sys.argv) > 2:
     head, rand = out[0], out.get(1)
     rd, wr = hbm_bytes(head)
     summary = {
-        "kernel": "stage_decompress_kernel",
+        "kernel": "+".join(KERNELS),
+        "decoder_src_sha": __import__("importlib").import_module("bench").decoder_src_sha(),
         "command": "bench.py (config 2 workload) under rocprofv3 --pmc, one counter group per pass (tools/pmc_bench.sh)",
         "blocks": int(sys.argv[3]) if len(sys.argv) > 3 else 1048576,
         "pool": int(sys.argv[4]) if len(sys.argv) > 4 else 4096,
