@@ -230,6 +230,23 @@ int lz4m_compress_block_api(const char* src, char* dst, int srcSize, int dstCapa
 uint32_t lz4m_xxh32(const void* input, size_t length, uint32_t seed);
 
 /*
+ * Streaming XXH32 on the HOST CPU (xxhash.c:437-554, XXH32_reset / _update /
+ * _digest; state fields as xxhash.h:264-274).  The frame content checksum is
+ * one serial XXH32 stream over all uncompressed bytes (lz4frame.c:1041-1042,
+ * :1170-1176, decode :1850, :1961): four multiply-rotate recurrences with no
+ * associative combine, so a GPU cannot split it (lz4m_xxh32_long runs it on
+ * one wavefront).  lz4.frame runs it here, on a host core, beside the device
+ * work.  Pure host code: no device, no allocation.
+ */
+typedef struct {
+    uint32_t total_len_32, large_len, v[4], mem32[4], memsize, reserved;
+} lz4m_xxh32_state;
+void lz4m_xxh32_host_reset(lz4m_xxh32_state* state, uint32_t seed);
+void lz4m_xxh32_host_update(lz4m_xxh32_state* state, const void* input, size_t length);
+uint32_t lz4m_xxh32_host_digest(const lz4m_xxh32_state* state);
+uint32_t lz4m_xxh32_host(const void* input, size_t length, uint32_t seed);
+
+/*
  * Block-record walk of an LZ4 frame already in device memory
  * (LZ4F_decompress, lz4frame.c:1643-1701 and 1926-1965): starting at the
  * first record (`pos` = header size), records k = 0.. get d_rec_pos[k] (the

@@ -9,12 +9,15 @@ LE32 block records); every byte-level operation runs on the GPU:
   launch with the LZ4_compress_fast_extState_fastReset parse
   (lz4frame.c:853-863 -> lz4.c:1378-1413, cap = block size - 1, raw block when
   it does not fit, lz4frame.c:834-842); block records are emitted by
-  ``lz4m_frame_emit`` at scanned offsets; the header checksum and the content
-  checksum (XXH32, lz4frame.c:341-345, 1042, 1171) run on the device.
+  ``lz4m_frame_emit`` at scanned offsets.  The content checksum (XXH32 over
+  all input, lz4frame.c:1042, 1171) is one serial stream: it runs on a host
+  core (lz4m_xxh32_host_*) in a thread beside the device work -- on the
+  caller's bytes, or on device bytes streamed back over PCIe in chunks; the
+  1-byte header checksum (lz4frame.c:341-345) too.
 * decompress: independent blocks decode in one batched launch into slots of
   the frame's maximum block size (the capacity LZ4F_decompress gives,
-  lz4frame.c:1844-1847), raw blocks are gathered, block checksums and the
-  content checksum are verified on the device.  Linked-block frames decode
+  lz4frame.c:1844-1847), raw blocks are gathered, block checksums are
+  verified on the device, the content checksum on a host core.  Linked-block frames decode
   block after block on one wavefront with the previous output as prefix.
 
 Scope notes: ``block_linked=True`` frames are written with the
@@ -25,7 +28,9 @@ codec's scope.
 """
 from __future__ import annotations
 
+import os
 import struct
+import threading
 
 import torch
 
@@ -50,13 +55,45 @@ def _err(fn: str, code: str) -> RuntimeError:
     return RuntimeError(f"{fn} failed with code: ERROR_{code}")
 
 
+def _content_on_gpu() -> bool:
+    """LZ4M_CONTENT_XXH32=gpu runs the content checksum on one wavefront
+    (lz4m_xxh32_long, 1.7 GB/s) instead of a host core (A/B runs)."""
+    return os.environ.get("LZ4M_CONTENT_XXH32", "host") == "gpu"
+
+
 def _xxh32_dev(buf: bytes | memoryview | torch.Tensor, n: int | None = None, seed: int = 0) -> int:
-    dev = N.device()
-    t = buf if isinstance(buf, torch.Tensor) else N.to_device(buf, dev, pad=1)
-    length = n if n is not None else (t.numel() if isinstance(buf, torch.Tensor) else memoryview(buf).nbytes)
-    out = torch.empty(1, dtype=torch.int32, device=t.device)
-    N.launch_xxh32_long(t, length, seed, out)
+    """XXH32 of a buffer: host bytes on this core; device bytes on a host
+    core over pipelined PCIe copies (or on the GPU, _content_on_gpu)."""
+    if not isinstance(buf, torch.Tensor):
+        return N.xxh32_host(buf, seed)
+    length = n if n is not None else buf.numel()
+    if not _content_on_gpu():
+        return N.xxh32_of_device(buf, length, seed)
+    out = torch.empty(1, dtype=torch.int32, device=buf.device)
+    N.launch_xxh32_long(buf, length, seed, out)
     return int(out.item()) & 0xFFFFFFFF
+
+
+class _HashThread(threading.Thread):
+    """The content checksum on a host core beside the device work."""
+
+    def __init__(self, fn):
+        super().__init__(daemon=True)
+        self._fn = fn
+        self.value = None
+        self.error = None
+
+    def run(self):
+        try:
+            self.value = self._fn()
+        except BaseException as e:   # re-raised in the caller
+            self.error = e
+
+    def result(self) -> int:
+        self.join()
+        if self.error is not None:
+            raise self.error
+        return self.value
 
 
 # ------------------------------------------------------------------ header
@@ -152,9 +189,9 @@ def compress(data, compression_level=0, block_size=0, content_checksum=False, bl
     bsid_req = _c_int(block_size, "block_size")
     dev = N.device()
     d_src = N.to_device(src, dev, pad=1)
-    frame = compress_device(d_src, src.nbytes, compression_level=level, block_size=bsid_req,
+    frame = _compress_frame(d_src, src.nbytes, compression_level=level, block_size=bsid_req,
                             content_checksum=content_checksum, block_checksum=block_checksum,
-                            block_linked=block_linked, store_size=store_size)
+                            block_linked=block_linked, store_size=store_size, host_src=src)[0]
     out = frame.cpu().numpy().tobytes()
     return bytearray(out) if return_bytearray else out
 
@@ -171,14 +208,16 @@ def compress_device(d_src: torch.Tensor, n: int | None = None, *, compression_le
     ratio of LZ4_compress_default, not byte-identical; BASELINE config 4).
 
     The content checksum (one serial XXH32 stream over all of d_src) runs on
-    its own stream beside the block compression."""
+    a host core beside the block compression, over pipelined PCIe copies of
+    d_src."""
     return _compress_frame(d_src, n, compression_level=compression_level, block_size=block_size,
                            content_checksum=content_checksum, block_checksum=block_checksum,
                            block_linked=block_linked, store_size=store_size, parse=parse, stream=stream)[0]
 
 
 def _compress_frame(d_src, n=None, *, compression_level=0, block_size=0, content_checksum=False,
-                    block_checksum=False, block_linked=True, store_size=True, parse="exact", stream=None):
+                    block_checksum=False, block_linked=True, store_size=True, parse="exact", stream=None,
+                    host_src=None):
     """compress_device, also returning the block records:
     (frame, {"data_off", "stored_len", "raw"}) with device tensors giving, per
     block, the payload position in the frame, its stored length and whether
@@ -205,13 +244,20 @@ def _compress_frame(d_src, n=None, *, compression_level=0, block_size=0, content
     body = None
     meta = None
     main = stream if stream is not None else torch.cuda.current_stream(dev)
-    h = None
+    h = hthread = None
     if content_checksum:                                       # lz4frame.c:1042, 1170-1176
-        side = torch.cuda.Stream(dev)
-        side.wait_stream(main)
-        h = torch.empty(1, dtype=torch.int32, device=dev)
-        N.launch_xxh32_long(d_src, n, 0, h, side)
-        h.record_stream(main)
+        if _content_on_gpu():
+            side = torch.cuda.Stream(dev)
+            side.wait_stream(main)
+            h = torch.empty(1, dtype=torch.int32, device=dev)
+            N.launch_xxh32_long(d_src, n, 0, h, side)
+            h.record_stream(main)
+        elif host_src is not None:   # the caller's bytes: hash them while the device compresses
+            hthread = _HashThread(lambda: N.xxh32_host(host_src))
+            hthread.start()
+        else:                        # device bytes: streamed back and hashed while the device compresses
+            hthread = _HashThread(lambda: N.xxh32_of_device(d_src, n, wait_stream=main))
+            hthread.start()
     if nb:
         raw_off = torch.arange(nb, dtype=torch.int64, device=dev) * bsize
         raw_len = torch.full((nb,), bsize, dtype=torch.int32, device=dev)
@@ -243,8 +289,12 @@ def _compress_frame(d_src, n=None, *, compression_level=0, block_size=0, content
     pos = len(hdr) + total
     out[pos: pos + 4] = 0                                      # endmark, lz4frame.c:1167
     if content_checksum:
-        main.wait_stream(side)
-        out[pos + 4: pos + 8] = h.view(torch.uint8)
+        if hthread is not None:
+            dig = hthread.result()
+            out[pos + 4: pos + 8] = torch.frombuffer(bytearray(struct.pack("<I", dig)), dtype=torch.uint8).to(dev)
+        else:
+            main.wait_stream(side)
+            out[pos + 4: pos + 8] = h.view(torch.uint8)
     return out[: pos + tail], meta
 
 
@@ -312,12 +362,12 @@ def decompress(data, return_bytearray=False, return_bytes_read=False):
             t([r[0] for r in recs], torch.bool), t([r[3] for r in recs], torch.int64))
     _frame_errors(first_err, state, info, total)
     bytes_read = state[1]
-    if info["content_checksum"]:
+    out = N.to_host_bytes(out_t, total, bool(return_bytearray)) if total else (bytearray() if return_bytearray else b"")
+    if info["content_checksum"]:   # on the host copy the caller gets (lz4frame.c:1850, :1959-1964)
         want = struct.unpack_from("<I", mv, state[2])[0]
-        got = _xxh32_dev(out_t, total) if total else _xxh32_dev(b"")
+        got = _xxh32_dev(out_t, total) if (total and _content_on_gpu()) else N.xxh32_host(out)
         if got != want:
             raise _err("LZ4F_decompress", "contentChecksum_invalid")
-    out = N.to_host_bytes(out_t, total, bool(return_bytearray)) if total else (bytearray() if return_bytearray else b"")
     if return_bytes_read:
         return out, bytes_read
     return out
@@ -329,9 +379,10 @@ def decompress_device(d_frame: torch.Tensor, n: int | None = None, stream=None) 
     the data (BASELINE config 4).  The header is parsed on
     the host from its first bytes; the block records are walked on the device
     (lz4m_frame_scan); independent blocks decode in one batched launch, linked
-    ones on the chain kernel; block and content checksums are verified on the
-    device.  A malformed or truncated frame raises exactly what
-    ``decompress`` raises for the same bytes."""
+    ones on the chain kernel; block checksums are verified on the device, the
+    content checksum on a host core over pipelined PCIe copies of the output.
+    A malformed or truncated frame raises exactly what ``decompress`` raises
+    for the same bytes."""
     n = d_frame.numel() if n is None else int(n)
     dev = d_frame.device
     head = bytes(d_frame[: min(n, 19)].cpu().numpy().tobytes())

@@ -132,3 +132,40 @@ def test_hot_kernels_use_no_scratch():
                 assert int(m.group(1)) == 0, f"{name} uses {m.group(1)} B/lane of scratch"
                 seen += 1
     assert seen >= 8
+
+
+def test_host_xxh32_matches_oracle_and_golden():
+    """The host streaming XXH32 of the C-ABI (the frame content checksum,
+    lz4m_xxh32_host_*) equals the oracle and the golden XXH32 values, for any
+    chunking of the stream (xxhash.c:437-554)."""
+    import json
+    import random
+
+    import numpy as np
+    import oracle as O
+    from conftest import GOLDEN
+    from lz4 import _native as N
+    orc = O.Oracle()
+    rnd = random.Random(7)
+    for n in [0, 1, 3, 4, 15, 16, 17, 31, 32, 33, 255, 4096, 65536 + 3]:
+        b = rnd.randbytes(n)
+        for seed in (0, 1, 0x9E3779B1):
+            assert N.xxh32_host(b, seed) == orc.xxh32(b, seed)
+            h = N.HostXXH32(seed)
+            pos = 0
+            while pos < n:
+                k = rnd.randrange(1, 40)
+                h.update(b[pos:pos + k])
+                pos += k
+            assert h.digest() == orc.xxh32(b, seed)
+    man = json.load(open(os.path.join(GOLDEN, "manifest.json")))
+    arr = np.load(os.path.join(GOLDEN, "golden.npz"), allow_pickle=False)
+    inputs = {e["name"]: arr[e["key"]].tobytes() for e in man["inputs"]}
+    checked = 0
+    for e in man["xxh32"]:
+        data = inputs.get(e.get("input")) if "input" in e else arr[e["key"]].tobytes() if "key" in e else None
+        if data is None:
+            continue
+        assert N.xxh32_host(data, e.get("seed", 0)) == e["value"], e
+        checked += 1
+    assert checked > 0

@@ -6,7 +6,7 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout
 rc=$?
 echo "tests rc=$rc"; tail -3 gpurun_out/gputests.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-timeout -k 10 600 python -u bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err
+timeout -k 10 700 python -u bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err
 rc2=$?
 echo "bench rc=$rc2"; tail -3 gpurun_out/bench.err; cat gpurun_out/bench.json
 exit $rc2
