@@ -1234,10 +1234,11 @@ __global__ __launch_bounds__(256, 4) void hist_decompress_kernel(const uint8_t* 
         }
         const bool fast = oend >= 64;
         int32_t ip = 0, op = 0, base = 0, F = 0, ib = -kCoopIn;
+        bool fit_cut = false;   // the last round stopped at a sequence that only did not fit the buffer
         HP_MARK(15);
         while (fast) {
             HP_COUNT(8, 1);
-            if (op - base > kHistRebase) {   // keep the last kHistKeep bytes
+            if (op - base > kHistRebase || (fit_cut && op - base > kHistKeep)) {   // keep the last kHistKeep bytes
                 const int32_t nb = (op - kHistKeep) & ~15;
                 // the move distance (> 2 KiB) exceeds the 1 KiB a wave moves per pass
                 for (int32_t c = 16 * (int32_t)lane; c < op - nb; c += 16 * kWave) {
@@ -1366,11 +1367,17 @@ __global__ __launch_bounds__(256, 4) void hist_decompress_kernel(const uint8_t* 
             // the reference's fast-loop margins (lz4.c:2004-2110, as fast_seq / decode_step)
             const bool lit_ok = q.litx ? ib + q.litpos + lit <= iend - 32 && o + lit <= oend - 32
                                        : sabs + 1 <= iend - 17;
-            const bool ok = act && q.simple && lit_ok && (!q.mlx || sabs + adv <= iend - 4) && off >= 1 &&
-                            off <= o + lit && o + len < oend - 64 && o + len <= base + kHistW;
+            const bool ok_nofit = act && q.simple && lit_ok && (!q.mlx || sabs + adv <= iend - 4) && off >= 1 &&
+                                  off <= o + lit && o + len < oend - 64;
+            const bool ok = ok_nofit && o + len <= base + kHistW;
             const uint64_t bad = __ballot(act) & ~__ballot(ok);
             const int use = bad ? __builtin_ctzll(bad) : nseq;
-            if (use == 0) break;
+            // a round cut only because the buffer is full goes on after a rebase;
+            // margins and errors go to the exact path
+            const bool fit_only = bad && ((__ballot(ok_nofit) >> use) & 1ull);
+            if (use == 0 && !(fit_only && !fit_cut && op - base > kHistKeep)) break;
+            fit_cut = fit_only;
+            if (use == 0) continue;
             HP_COUNT(10, use);
             HP_MARK(2);
             const bool u = (int)lane < use;
@@ -1435,7 +1442,7 @@ __global__ __launch_bounds__(256, 4) void hist_decompress_kernel(const uint8_t* 
                 st16(d + c, lds_ld16(OB + (c - base)));
             F += (op - F) & ~15;
             HP_MARK(5);
-            if (use < nseq) break;
+            if (use < nseq && !fit_only) break;
         }
         // flush the rest exactly, then the exact state machine from (ip, op)
         for (int32_t c = F + 16 * (int32_t)lane; c < op; c += 16 * kWave)

@@ -398,3 +398,32 @@ def test_host_single_block_functions(gpu, oracle, corpus):
     bad[len(bad) // 2] ^= 0xFF
     assert lib.lz4m_decompress_safe(bytes(bad), dec, len(bad), len(b)) == \
         oracle.decompress(bytes(bad), len(b))[0]
+
+
+def _phrases(n_bytes: int, seed: int) -> bytes:
+    """High-ratio data made of 60-250 byte slices of a small vocabulary: LZ4
+    matches of ~60-250 bytes, ~90 decoded bytes per sequence."""
+    rng = np.random.default_rng(seed)
+    vocab = rng.integers(0, 256, size=(64, 400), dtype=np.uint8)
+    out, total = [], 0
+    while total < n_bytes:
+        L = int(rng.integers(60, 251))
+        w = vocab[int(rng.integers(0, 64))]
+        a = int(rng.integers(0, 400 - L))
+        out.append(w[a:a + L].tobytes())
+        total += L
+    return b"".join(out)[:n_bytes]
+
+
+@pytest.mark.parametrize("decoder", DECODERS)
+@pytest.mark.parametrize("block", [65536, 4 << 20])
+def test_decompress_high_ratio(gpu, oracle, decoder, block):
+    """Mid-length matches (60-250 B, ~90 B per sequence): rounds of the
+    on-chip-history decoders fill their buffers long before 64 sequences, so
+    a round cut by buffer space must go on after a rebase, and
+    the output must still equal the oracle's."""
+    blocks = [_phrases(block, 40 + i) for i in range(3 if block > 65536 else 24)]
+    comp = [oracle.compress(b) for b in blocks]
+    got = gpu_decompress(comp, [block] * len(blocks), gpu, decoder)
+    for (st, out), b in zip(got, blocks):
+        assert st == len(b) and out == b
