@@ -7,9 +7,10 @@
  * points replace those calls with stream-ordered, batched HIP launches over
  * device-resident blocks.  Plain pointers and sizes only: every pointer named
  * d_* is a device (HBM) pointer, `stream` is a hipStream_t.  No batched entry
- * point synchronises or touches host memory; only lz4m_decompress_batch
- * allocates (64 bytes, stream-ordered), so every call can be captured into a
- * hipGraph.
+ * point synchronises or touches host memory except the speculative mode of
+ * lz4m_compress_linked_batch (one stream synchronisation per pass); only
+ * lz4m_decompress_batch allocates (64 bytes, stream-ordered), so every other
+ * call can be captured into a hipGraph.
  *
  * Return value of every launcher: 0 on success, otherwise a hipError_t value
  * (launch failure) or LZ4M_EINVAL (bad argument).
@@ -58,6 +59,49 @@ typedef struct ihipStream_t* lz4m_stream_t;   /* == hipStream_t */
 
 /* LZ4_compressBound (lz4.h:212 / lz4.c:730). */
 int lz4m_compress_bound(int input_size);
+
+/*
+ * Batched lz4.block.compress(source, dict=D) for the non-HC modes
+ * (_block.c:93-107: LZ4_resetStream + LZ4_loadDict, lz4.c:1541-1581, +
+ * LZ4_compress_fast_continue, lz4.c:1632-1708), byte-identical.
+ * d_dict_len[i] < 0: no dictionary (same as lz4m_compress_batch with
+ * LZ4M_TABLE_U32_HASH5).  d_dict_len[i] >= 0: the dictionary's full length;
+ * its last min(d_dict_len[i], 65536) bytes must be stored immediately before
+ * block i in d_src (d_src + d_src_off[i] - that many bytes).  Like
+ * LZ4_loadDict, a dictionary shorter than 8 bytes is not used as history but
+ * still changes the parse (an empty dict= differs from no dict=).
+ */
+int lz4m_compress_dict_batch(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len,
+                             const int32_t* d_dict_len, uint8_t* d_dst, const int64_t* d_dst_off,
+                             const int32_t* d_dst_cap, int32_t* d_out_len, int64_t n, int acceleration,
+                             lz4m_stream_t stream);
+
+/*
+ * Batched linked-block compression: the blocks of one stream are compressed
+ * as consecutive LZ4_compress_fast_continue calls on one LZ4_stream_t that
+ * was freshly initialised (LZ4F_compressBlock_continue, lz4frame.c:865-871;
+ * LZ4F_compressFrame with blockLinked), byte-identical to the reference.
+ * d_link[i] = 0 starts a new stream at block i, 1 continues the stream of
+ * block i-1, whose bytes must end where block i starts in d_src.  Capacities
+ * < LZ4_compressBound select limitedOutput (0 = did not fit; the frame stores
+ * such a block raw, lz4frame.c:833-842, and the stream still continues).
+ *   LZ4M_LINKED_SERIAL: one wavefront per stream, no scratch, stream-ordered.
+ *   LZ4M_LINKED_SPECULATIVE: one wavefront per block, parallel within a
+ *     stream (every block compressed from its predecessor's table,
+ *     speculatively, in passes until no table changes).  Every block that has
+ *     a successor in its stream must be >= 65536 B (frame blocks are; else
+ *     LZ4M_EINVAL).  Needs lz4m_compress_linked_workspace_size(n) bytes of
+ *     device scratch and SYNCHRONISES the stream once per pass (typically 3-6).
+ */
+#define LZ4M_LINKED_SERIAL      1
+#define LZ4M_LINKED_SPECULATIVE 2
+size_t lz4m_compress_linked_workspace_size(int64_t n);
+/* passes the calling thread's last speculative call took (diagnostics) */
+int lz4m_compress_linked_passes(void);
+int lz4m_compress_linked_batch(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len,
+                               const int32_t* d_link, uint8_t* d_dst, const int64_t* d_dst_off,
+                               const int32_t* d_dst_cap, int32_t* d_out_len, int64_t n, int acceleration,
+                               int mode, void* d_work, size_t work_bytes, lz4m_stream_t stream);
 
 /* Library identification (mirrors LZ4_versionNumber, lz4.c:728, of the
  * format version this codec is bit-compatible with: 10904). */

@@ -206,6 +206,193 @@ int orc_compress_block_api(const uint8_t* src, uint8_t* dst, int n, int cap, int
     return orc_compress(src, n, dst, cap, ORC_TABLE_U32_HASH5, accel);
 }
 
+/*
+ * Greedy byU32 compressor of one block that has HISTORY: the streaming modes
+ * of LZ4_compress_fast_continue (lz4.c:1632-1708) restated over one
+ * contiguous window w[0 .. hist+n): history w[0 .. hist), block w[hist ..).
+ * The caller owns the 4096-entry table (carried across calls).
+ *
+ * A table entry is an index; window byte p has index ibase + p, so the block
+ * starts at index ibase + hist (the stream's currentOffset, lz4.c:925-926).
+ * Candidates with index < low_idx are outside the valid area (dictSmall,
+ * lz4.c:1061, 1247); candidates further than 65535 back are too far
+ * (lz4.c:1062-1065).  Backward catch-up (lz4.c:1080) stops at window byte
+ * low_src for matches inside the block and low_dict for matches in the
+ * history (extDict sets lowLimit per candidate, lz4.c:1036-1053; prefix mode
+ * fixes it at source - dictSize, lz4.c:966).  A match that runs off the end
+ * of the history continues into the block (lz4.c:1141-1153), which the
+ * contiguous window gives for free.
+ *
+ * The three python-lz4 callers:
+ *   lz4.block.compress(dict=D), |D| >= 8   (_block.c:101-104 -> LZ4_loadDict,
+ *     lz4.c:1541-1581, then usingExtDict): window = last min(|D|,64K) bytes
+ *     of D + block, ibase = 65536 - hist, low_idx = ibase, low_src = hist,
+ *     low_dict = 0;
+ *   lz4.block.compress(dict=D), |D| < 8    (LZ4_loadDict keeps no dictionary,
+ *     prefix mode with dictSmall): hist = 0, ibase = low_idx = 65536;
+ *   linked frame blocks (lz4frame.c:865-871, prefix mode over the frame):
+ *     window = frame start, hist = block offset, ibase = low_* = 0.
+ */
+int orc_compress_window(const uint8_t* w, int64_t hist, int n, uint8_t* dst, int cap, int accel,
+                        uint32_t* table, uint32_t ibase, uint32_t low_idx, int64_t low_src,
+                        int64_t low_dict)
+{
+    static const int kSkipTrigger = 6;
+    const uint8_t* const src = w + hist;
+    const uint8_t* const iend = src + n;
+    const uint8_t* const mflimit1 = iend - ORC_MFLIMIT + 1;
+    const uint8_t* const matchlimit = iend - ORC_LASTLITERALS;
+    const uint8_t* anchor = src;
+    const uint8_t* ip = src;
+    uint8_t* op = dst;
+    uint8_t* const olimit = dst + cap;
+    const int limited = cap < orc_compress_bound(n);
+    const uint32_t start_idx = ibase + (uint32_t)hist;
+    uint32_t fwd_h;
+
+    if ((unsigned)n > (unsigned)ORC_MAX_INPUT) return 0;
+    if (accel < 1) accel = 1;
+    if (accel > ORC_ACCEL_MAX) accel = ORC_ACCEL_MAX;
+    if (n == 0) {
+        if (limited && cap <= 0) return 0;
+        dst[0] = 0;
+        return 1;
+    }
+    if (n < ORC_MIN_LENGTH) goto last_literals;
+
+    table[orc_hash(ip, ORC_TABLE_U32_HASH5)] = start_idx;          /* lz4.c:984 */
+    ip++;
+    fwd_h = orc_hash(ip, ORC_TABLE_U32_HASH5);
+
+    for (;;) {
+        const uint8_t* match;
+        uint8_t* token;
+        {
+            const uint8_t* fwd = ip;
+            int step = 1;
+            int attempts = accel << kSkipTrigger;
+            for (;;) {
+                const uint32_t h = fwd_h;
+                const uint32_t cur = ibase + (uint32_t)(fwd - w);
+                const uint32_t cand = table[h];
+                ip = fwd;
+                fwd += step;
+                step = attempts++ >> kSkipTrigger;
+                if (fwd > mflimit1) goto last_literals;
+                fwd_h = orc_hash(fwd, ORC_TABLE_U32_HASH5);
+                table[h] = cur;
+                if (cand < low_idx) continue;                      /* lz4.c:1061 */
+                if (cand + ORC_DIST_MAX < cur) continue;           /* lz4.c:1062-1065 */
+                match = w + (int64_t)(cand - ibase);
+                if (orc_rd32(match) == orc_rd32(ip)) break;
+            }
+        }
+        {   /* catch-up with the lowLimit of the match's segment */
+            const uint8_t* const low = w + (match < src ? low_dict : low_src);
+            while (ip > anchor && match > low && ip[-1] == match[-1]) { ip--; match--; }
+        }
+        {
+            const unsigned lit = (unsigned)(ip - anchor);
+            token = op++;
+            if (limited && op + lit + (2 + 1 + ORC_LASTLITERALS) + lit / 255 > olimit) return 0;
+            if (lit >= 15) { *token = 15 << 4; op = orc_put_len(op, lit - 15); }
+            else *token = (uint8_t)(lit << 4);
+            memcpy(op, anchor, lit);
+            op += lit;
+        }
+next_match:
+        {
+            const unsigned off = (unsigned)(ip - match);
+            unsigned mcode;
+            op[0] = (uint8_t)off; op[1] = (uint8_t)(off >> 8); op += 2;
+            mcode = orc_count(ip + ORC_MINMATCH, match + ORC_MINMATCH, matchlimit);
+            ip += mcode + ORC_MINMATCH;
+            if (limited && op + (1 + ORC_LASTLITERALS) + (mcode + 240) / 255 > olimit) return 0;
+            if (mcode >= 15) { *token += 15; op = orc_put_len(op, mcode - 15); }
+            else *token += (uint8_t)mcode;
+        }
+        anchor = ip;
+        if (ip >= mflimit1) break;
+        table[orc_hash(ip - 2, ORC_TABLE_U32_HASH5)] = ibase + (uint32_t)(ip - 2 - w);
+        {
+            const uint32_t h = orc_hash(ip, ORC_TABLE_U32_HASH5);
+            const uint32_t cur = ibase + (uint32_t)(ip - w);
+            const uint32_t cand = table[h];
+            table[h] = cur;
+            if (cand >= low_idx && cand + ORC_DIST_MAX >= cur) {
+                match = w + (int64_t)(cand - ibase);
+                if (orc_rd32(match) == orc_rd32(ip)) {
+                    token = op++;
+                    *token = 0;
+                    goto next_match;
+                }
+            }
+        }
+        fwd_h = orc_hash(++ip, ORC_TABLE_U32_HASH5);
+    }
+last_literals:
+    {
+        const size_t run = (size_t)(iend - anchor);
+        if (limited && op + run + 1 + (run + 255 - 15) / 255 > olimit) return 0;
+        if (run >= 15) { *op++ = 15 << 4; op = orc_put_len(op, (unsigned)(run - 15)); }
+        else *op++ = (uint8_t)(run << 4);
+        memcpy(op, anchor, run);
+        op += run;
+    }
+    (void)start_idx;
+    return (int)(op - dst);
+}
+
+/* lz4.block.compress(source, dict=D) for a non-HC mode (_block.c:93-107):
+ * LZ4_resetStream, LZ4_loadDict (lz4.c:1541-1581: last 64 KiB of D, every
+ * third position hashed, indexes ending at 64 KiB), LZ4_compress_fast_continue.
+ * `win` holds the last min(d_len, 65536) bytes of D followed by the source. */
+int orc_compress_dict(const uint8_t* win, int64_t d_len, int n, uint8_t* dst, int cap, int accel)
+{
+    uint32_t table[4096];
+    memset(table, 0, sizeof(table));
+    if (d_len < 8)                                                 /* lz4.c:1564-1566 */
+        return orc_compress_window(win, 0, n, dst, cap, accel, table, 65536, 65536, 0, 0);
+    {
+        const int64_t dt = d_len > 65536 ? 65536 : d_len;
+        const uint32_t ibase = (uint32_t)(65536 - dt);
+        int64_t p;
+        for (p = 0; p <= dt - 8; p += 3)                           /* lz4.c:1575-1578 */
+            table[orc_hash(win + p, ORC_TABLE_U32_HASH5)] = ibase + (uint32_t)p;
+        return orc_compress_window(win, dt, n, dst, cap, accel, table, ibase, ibase, dt, 0);
+    }
+}
+
+/* The blocks of one linked frame (LZ4F_compressFrame with blockLinked,
+ * lz4frame.c:865-871 + 960-1001): one stream, LZ4_compress_fast_continue per
+ * block straight from the contiguous source, dstCapacity = blockSize - 1
+ * (lz4frame.c:835).  out_len[k] = compressed size, 0 = stored raw.  The
+ * 2 GB index renormalisation (LZ4_renormDictT, lz4.c:1612-1630) is restated
+ * as a window shift; it never changes a parse. */
+int orc_compress_linked(const uint8_t* src, int64_t n, int bsize, int accel, uint8_t* dst,
+                        int64_t dst_stride, int32_t* out_len)
+{
+    uint32_t table[4096];
+    const uint8_t* w = src;
+    int64_t pos = 0, k = 0;
+    uint32_t start = 0;
+    memset(table, 0, sizeof(table));
+    for (; pos < n; pos += bsize, ++k) {
+        const int len = (int)(n - pos < bsize ? n - pos : bsize);
+        if ((uint64_t)start + (uint64_t)len > 0x80000000ull) {
+            const uint32_t delta = start - 65536;
+            int i;
+            for (i = 0; i < 4096; i++) table[i] = table[i] < delta ? 0 : table[i] - delta;
+            w += delta;
+            start = 65536;
+        }
+        out_len[k] = orc_compress_window(w, (int64_t)(src + pos - w), len, dst + k * dst_stride, len - 1,
+                                         accel, table, 0, 0, 0, 0);
+        start += (uint32_t)len;
+    }
+    return (int)k;
+}
+
 /* read_variable_length (lz4.c:1903-1928).  Returns 0 on success. */
 static int orc_read_len(const uint8_t** ipp, const uint8_t* ilimit, int initial_check, size_t* out)
 {

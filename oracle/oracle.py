@@ -68,6 +68,10 @@ class Oracle:
         lib.orc_xxh32_digest.restype = C.c_uint32
         lib.orc_compress_batch.argtypes = [vp, vp, vp, vp, vp, C.c_int32, vp, i64, i32, i32]
         lib.orc_decompress_batch.argtypes = [vp, vp, vp, vp, vp, vp, vp, i64]
+        lib.orc_compress_dict.argtypes = [vp, i64, i32, vp, i32, i32]
+        lib.orc_compress_dict.restype = i32
+        lib.orc_compress_linked.argtypes = [vp, i64, i32, i32, vp, i64, vp]
+        lib.orc_compress_linked.restype = i32
         self.lib = lib
 
     def compress(self, data, variant: int | None = None, accel: int = 1, cap: int | None = None) -> bytes | None:
@@ -80,6 +84,28 @@ class Oracle:
         dst = np.zeros(max(cap, 1), dtype=np.uint8)
         r = self.lib.orc_compress(sp, n, dst.ctypes.data_as(C.c_void_p), cap, variant, accel)
         return None if r <= 0 else dst[:r].tobytes()
+
+    def compress_dict(self, data, dict_, accel: int = 1) -> bytes | None:
+        """lz4.block.compress(data, dict=dict_, store_size=False) (_block.c:93-107)."""
+        d = bytes(dict_)
+        tail = d[-65536:] if len(d) >= 8 else b""
+        win, wp = _buf(tail + bytes(data))
+        n = win.size - len(tail)
+        cap = compress_bound(n)
+        dst = np.zeros(max(cap, 1), dtype=np.uint8)
+        r = self.lib.orc_compress_dict(wp, len(d), n, dst.ctypes.data_as(C.c_void_p), cap, accel)
+        return None if r <= 0 else dst[:r].tobytes()
+
+    def compress_linked(self, data, block_size: int, accel: int = 1) -> list:
+        """Per-block payloads of a linked frame: bytes, or None = stored raw."""
+        src, sp = _buf(data)
+        nb = (src.size + block_size - 1) // block_size
+        stride = compress_bound(block_size)
+        dst = np.zeros(max(nb, 1) * stride, dtype=np.uint8)
+        out = np.zeros(max(nb, 1), dtype=np.int32)
+        self.lib.orc_compress_linked(sp, src.size, block_size, accel, dst.ctypes.data_as(C.c_void_p), stride,
+                                     out.ctypes.data_as(C.c_void_p))
+        return [dst[k * stride: k * stride + out[k]].tobytes() if out[k] > 0 else None for k in range(nb)]
 
     def decompress(self, data, cap: int, dict_=None) -> tuple[int, bytes]:
         src, sp = _buf(data)
@@ -126,6 +152,8 @@ class Reference:
         lib.LZ4_resetStream.argtypes = [vp]
         lib.LZ4_compress_fast_continue.argtypes = [vp, vp, vp, i32, i32, i32]
         lib.LZ4_compress_fast_continue.restype = i32
+        lib.LZ4_loadDict.argtypes = [vp, vp, i32]
+        lib.LZ4_loadDict.restype = i32
         lib.XXH32.argtypes = [vp, sz, C.c_uint32]
         lib.XXH32.restype = C.c_uint32
         lib.LZ4_versionNumber.restype = i32
@@ -154,6 +182,18 @@ class Reference:
         dst = np.zeros(cap, dtype=np.uint8)
         state = C.create_string_buffer(int(self.lib.LZ4_sizeofState()))
         self.lib.LZ4_resetStream(state)
+        r = self.lib.LZ4_compress_fast_continue(state, sp, dst.ctypes.data_as(C.c_void_p), src.size, cap, accel)
+        return dst[:r].tobytes()
+
+    def compress_dict(self, data, dict_, accel: int = 1) -> bytes:
+        """lz4.block.compress(data, dict=dict_, store_size=False): _block.c:93-107."""
+        src, sp = _buf(data)
+        d = np.frombuffer(bytes(dict_) + b"\0", dtype=np.uint8)   # never a NULL buffer, like Py_buffer
+        cap = compress_bound(src.size)
+        dst = np.zeros(max(cap, 1), dtype=np.uint8)
+        state = C.create_string_buffer(int(self.lib.LZ4_sizeofState()))
+        self.lib.LZ4_resetStream(state)
+        self.lib.LZ4_loadDict(state, d.ctypes.data_as(C.c_void_p), d.size - 1)
         r = self.lib.LZ4_compress_fast_continue(state, sp, dst.ctypes.data_as(C.c_void_p), src.size, cap, accel)
         return dst[:r].tobytes()
 

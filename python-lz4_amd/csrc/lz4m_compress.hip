@@ -43,6 +43,11 @@ __device__ __forceinline__ int64_t skip_sum(int64_t m) {
     return 32 * q * (q - 1) + q * (r + 1);
 }
 
+// offset from ip of search attempt k (lz4.c:1021-1027: step = attempts++ >> 6)
+__device__ __forceinline__ int64_t attempt_off(int64_t k, int64_t A, int64_t FA) {
+    return k >= 1 ? 1 + skip_sum(A + k - 2) - FA : 0;
+}
+
 template <int V>
 struct Table;
 
@@ -54,6 +59,14 @@ struct Table<LZ4M_TABLE_U16_HASH4> {   // 8192 x u16 (lz4.c:756-762, 839-843)
     }
     __device__ static __forceinline__ uint32_t get(const uint16_t* t, uint32_t h) { return t[h]; }
     __device__ static __forceinline__ void put(uint16_t* t, uint32_t h, uint32_t v) { t[h] = (uint16_t)v; }
+    // volatile: kept in program order, never forwarded (the probe reads back
+    // what OTHER lanes wrote)
+    __device__ static __forceinline__ uint32_t get_v(uint16_t* t, uint32_t h) {
+        return reinterpret_cast<volatile uint16_t*>(t)[h];
+    }
+    __device__ static __forceinline__ void put_v(uint16_t* t, uint32_t h, uint32_t v) {
+        reinterpret_cast<volatile uint16_t*>(t)[h] = (uint16_t)v;
+    }
     static constexpr bool kDistCheck = false;   // lz4.c:1064, LZ4_DISTANCE_MAX == 65535
 };
 
@@ -68,6 +81,12 @@ struct Table<LZ4M_TABLE_U32_HASH5> {   // 4096 x u32 (lz4.c:764-774, 834-838)
     }
     __device__ static __forceinline__ void put(uint16_t* t, uint32_t h, uint32_t v) {
         reinterpret_cast<uint32_t*>(t)[h] = v;
+    }
+    __device__ static __forceinline__ uint32_t get_v(uint16_t* t, uint32_t h) {
+        return reinterpret_cast<volatile uint32_t*>(t)[h];
+    }
+    __device__ static __forceinline__ void put_v(uint16_t* t, uint32_t h, uint32_t v) {
+        reinterpret_cast<volatile uint32_t*>(t)[h] = v;
     }
     static constexpr bool kDistCheck = true;
 };
@@ -103,9 +122,22 @@ __device__ __forceinline__ int64_t put_len(uint8_t* dst, int64_t op, int64_t len
     return op + n255 + 1;
 }
 
+// Window form.  The block is w[hist .. hist+n); w[0 .. hist) is history the
+// parse may match into (a dictionary or the previous blocks of a linked
+// frame).  Table entries are indexes: window byte p has index ibase + p, so
+// the block starts at index ibase + hist (the stream's currentOffset,
+// lz4.c:925-926).  A candidate below low_idx is outside the valid area
+// (dictSmall, lz4.c:1061/1247) and one more than 65535 back is too far
+// (lz4.c:1062-1065, byU32 only).  Backward catch-up stops at window byte
+// low_src for matches inside the block and low_dict for matches in the
+// history (lowLimit, lz4.c:966, 1036-1053).  The caller prepares the table
+// (zeroed for a fresh stream, lz4.c:1513 / LZ4_prepareTable; loaded from a
+// dictionary; or carried over from the previous block).
+// oracle: orc_compress_window (oracle/lz4_oracle.c).
 template <int V>
-__device__ int64_t compress_block(const uint8_t* __restrict__ src, int64_t n, uint8_t* dst, int64_t cap,
-                                  int accel, uint16_t* tab, uint32_t lane) {
+__device__ int64_t compress_block_w(const uint8_t* __restrict__ w, int64_t hist, int64_t n, uint8_t* dst,
+                                    int64_t cap, int accel, uint16_t* tab, uint32_t lane, uint32_t ibase,
+                                    uint32_t low_idx, int64_t low_src, int64_t low_dict) {
     using T = Table<V>;
     if (n > kMaxInput) return 0;                               // lz4.c:1324
     const bool limited = cap < bound64(n);
@@ -116,22 +148,18 @@ __device__ int64_t compress_block(const uint8_t* __restrict__ src, int64_t n, ui
     }
     if (V == LZ4M_TABLE_U16_HASH4 && n >= kLimit64K) return 0;   // lz4.c:963
 
-    const int64_t mflimit1 = n - 12 + 1;                        // lz4.c:942
-    const int64_t matchlimit = n - 5;
+    const int64_t iend = hist + n;
+    const int64_t mflimit1 = iend - 12 + 1;                     // lz4.c:942
+    const int64_t matchlimit = iend - 5;
     const int64_t A = (int64_t)accel << 6;                      // searchMatchNb start
     const int64_t FA = skip_sum(A - 1);
-    int64_t anchor = 0, ip = 0, op = 0;
+    int64_t anchor = hist, ip = hist, op = 0;
 
-    // fresh table (lz4.c:1513, 1522 / LZ4_prepareTable)
-    {
-        u32x4* t4 = reinterpret_cast<u32x4*>(tab);
-        for (int k = lane; k < 16384 / 16; k += kWave) t4[k] = u32x4{0, 0, 0, 0};
-        __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0)
-    }
     if (n < kMinLength) goto last_literals;                    // lz4.c:981
 
-    if (lane == 0) T::put(tab, T::hash(src), 0);               // lz4.c:984
-    ip = 1;
+    if (lane == 0) T::put(tab, T::hash(w + hist), ibase + (uint32_t)hist);   // lz4.c:984
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    ip = hist + 1;
 
     for (;;) {
         int64_t match;
@@ -140,47 +168,56 @@ __device__ int64_t compress_block(const uint8_t* __restrict__ src, int64_t n, ui
             int64_t k0 = 0;
             for (;;) {
                 const int64_t k = k0 + lane;
-                const int64_t pos = ip + (k >= 1 ? 1 + skip_sum(A + k - 2) - FA : 0);
+                const int64_t pos = ip + attempt_off(k, A, FA);
                 const int64_t nxt = ip + 1 + skip_sum(A + k - 1) - FA;   // position of attempt k+1
                 const bool valid = nxt <= mflimit1;
                 const uint64_t vmask = __ballot(valid);
                 const int nvalid = __builtin_popcountll(vmask);   // valid lanes are a prefix
-                uint32_t h = 0, old = 0;
+                const uint32_t cur = ibase + (uint32_t)pos;
+                // read the bucket, then probe it with the lane id: a lane that
+                // does not read its own id back shares its hash with another
+                // lane of this step (one LDS round trip, in order per wave)
+                uint32_t h = 0, old = 0, rb = lane;
                 if (valid) {
-                    h = T::hash(src + pos);
-                    old = T::get(tab, h);
-                    T::put(tab, h, lane);                      // collision probe
+                    h = T::hash(w + pos);
+                    old = T::get_v(tab, h);
+                    T::put_v(tab, h, lane);
+                    rb = T::get_v(tab, h);
                 }
-                __builtin_amdgcn_s_waitcnt(0xc07f);
-                bool dup = false;
-                if (valid) dup = T::get(tab, h) != lane;
-                int pred = -1;      // nearest earlier lane with the same hash
-                int succ = 1 << 20; // nearest later valid lane with the same hash (none: +inf)
-                if (__ballot(dup) != 0) {
-                    for (int d = 1; d < nvalid; ++d) {
-                        const uint32_t hu = __shfl_up(h, d);
-                        const uint32_t hd = __shfl_down(h, d);
-                        if (valid && (int)lane >= d && pred < 0 && hu == h) pred = (int)lane - d;
-                        if (valid && (int)lane + d < nvalid && succ == (1 << 20) && hd == h) succ = (int)lane + d;
+                // per hash group: nearest earlier (pred) and later (succ) lane
+                int pred = -1, succ = 1 << 20;
+                uint64_t todo = __ballot(rb != lane);
+                while (todo) {
+                    const int l = __builtin_ctzll(todo);
+                    const uint32_t h0 = (uint32_t)__builtin_amdgcn_readlane((int)h, l);
+                    const bool in = valid && h == h0;
+                    const uint64_t same = __ballot(in);
+                    todo &= ~same;
+                    if (in) {
+                        const uint64_t lt = same & ((1ull << lane) - 1ull);
+                        const uint64_t gt = lane == 63 ? 0ull : same & ~((2ull << lane) - 1ull);
+                        pred = lt ? 63 - __builtin_clzll(lt) : -1;
+                        succ = gt ? __builtin_ctzll(gt) : 1 << 20;
                     }
                 }
-                const int64_t pred_pos = __shfl(pos, pred < 0 ? (int)lane : pred);
-                const int64_t cand = pred >= 0 ? pred_pos : (int64_t)old;
+                // the serial loop inserted an earlier lane of the group first
+                const uint32_t cand = pred >= 0 ? ibase + (uint32_t)(ip + attempt_off(k0 + pred, A, FA)) : old;
+                int64_t cpos = pos;
                 bool hit = false;
                 if (valid) {
-                    const bool far = T::kDistCheck && cand + 65535 < pos;
-                    hit = !far && ld32(src + cand) == ld32(src + pos);
+                    const bool bad = (T::kDistCheck && cand + 65535u < cur) || cand < low_idx;
+                    cpos = bad ? pos : (int64_t)cand - (int64_t)ibase;
+                    hit = !bad && ld32(w + cpos) == ld32(w + pos);
                 }
                 const uint64_t hmask = __ballot(hit);
                 const int f = hmask ? __builtin_ctzll(hmask) : nvalid;   // last lane processed: f (or all valid)
-                // restore lanes after f, then commit lanes <= f (last writer wins)
-                if (valid && (int)lane > f) T::put(tab, h, old);
-                __builtin_amdgcn_s_waitcnt(0xc07f);
-                if (valid && (int)lane <= f && (succ > f)) T::put(tab, h, (uint32_t)pos);
-                __builtin_amdgcn_s_waitcnt(0xc07f);
+                // one write per touched bucket: the group's last lane <= f
+                // inserts its position; a group entirely after f restores
+                if (valid && (((int)lane <= f && succ > f) || ((int)lane > f && pred < 0)))
+                    T::put_v(tab, h, (int)lane <= f ? cur : old);
                 if (hmask) {
-                    ip = __shfl(pos, f);
-                    match = __shfl(cand, f);
+                    ip = readlane64(pos, f);
+                    match = readlane64(cpos, f);
                     break;
                 }
                 if (nvalid < kWave) goto last_literals;        // forwardIp > mflimitPlusOne
@@ -191,9 +228,10 @@ __device__ int64_t compress_block(const uint8_t* __restrict__ src, int64_t n, ui
         }
 
         {   // ---- backward catch-up (lz4.c:1080) ----
+            const int64_t low = match < hist ? low_dict : low_src;
             for (;;) {
                 const int64_t a = ip - 1 - lane, b = match - 1 - lane;
-                const bool ok = a >= anchor && b >= 0 && src[a < 0 ? 0 : a] == src[b < 0 ? 0 : b];
+                const bool ok = a >= anchor && b >= low && w[a < 0 ? 0 : a] == w[b < 0 ? 0 : b];
                 const uint64_t m = __ballot(ok);
                 const int run = ~m == 0 ? kWave : (int)__builtin_ctzll(~m);   // leading lanes that extend
                 ip -= run;
@@ -213,7 +251,7 @@ __device__ int64_t compress_block(const uint8_t* __restrict__ src, int64_t n, ui
             } else if (lane == 0) {
                 dst[tok_pos] = (uint8_t)(lit << 4);
             }
-            wave_copy(dst + op, src + anchor, lit, cap - op, n - anchor, lane);
+            wave_copy(dst + op, w + anchor, lit, cap - op, iend - anchor, lane);
             op += lit;
         }
 
@@ -225,7 +263,8 @@ __device__ int64_t compress_block(const uint8_t* __restrict__ src, int64_t n, ui
                 dst[op + 1] = (uint8_t)(off >> 8);
             }
             op += 2;
-            // LZ4_count(ip+4, match+4, matchlimit), 4 bytes per lane
+            // LZ4_count(ip+4, match+4, matchlimit), 4 bytes per lane; a match
+            // in the history runs on into the block (lz4.c:1141-1153)
             int64_t mcode = 0;
             const int64_t p = ip + 4, q = match + 4;
             for (;;) {
@@ -235,13 +274,13 @@ __device__ int64_t compress_block(const uint8_t* __restrict__ src, int64_t n, ui
                 uint32_t x = 0xFFFFFFFFu;   // nonzero = mismatch within range
                 int lim = 0;
                 if (rem >= 4) {
-                    x = ld32(src + p + at) ^ ld32(src + q + at);
+                    x = ld32(w + p + at) ^ ld32(w + q + at);
                     lim = 4;
                 } else if (rem > 0) {
                     uint32_t xa = 0, xb = 0;
                     for (int j = 0; j < (int)rem; ++j) {
-                        xa |= (uint32_t)src[p + at + j] << (8 * j);
-                        xb |= (uint32_t)src[q + at + j] << (8 * j);
+                        xa |= (uint32_t)w[p + at + j] << (8 * j);
+                        xb |= (uint32_t)w[q + at + j] << (8 * j);
                     }
                     x = xa ^ xb;
                     lim = (int)rem;
@@ -258,7 +297,7 @@ __device__ int64_t compress_block(const uint8_t* __restrict__ src, int64_t n, ui
                     continue;
                 }
                 const int fl = __builtin_ctzll(stop);
-                mcode += 4 * (int64_t)fl + __shfl(eq, fl);
+                mcode += 4 * (int64_t)fl + __builtin_amdgcn_readlane(eq, fl);
                 break;
             }
             mcode = uni64(mcode);
@@ -277,16 +316,18 @@ __device__ int64_t compress_block(const uint8_t* __restrict__ src, int64_t n, ui
         if (ip >= mflimit1) break;                             // lz4.c:1204
 
         {   // ---- fill table, test next position (lz4.c:1207-1258) ----
-            if (lane == 0) T::put(tab, T::hash(src + ip - 2), (uint32_t)(ip - 2));
+            if (lane == 0) T::put(tab, T::hash(w + ip - 2), ibase + (uint32_t)(ip - 2));
             __builtin_amdgcn_s_waitcnt(0xc07f);
-            const uint32_t h = T::hash(src + ip);
+            const uint32_t h = T::hash(w + ip);
             const uint32_t cand = uni(T::get(tab, h));
+            const uint32_t cur = ibase + (uint32_t)ip;
             __builtin_amdgcn_s_waitcnt(0xc07f);
-            if (lane == 0) T::put(tab, h, (uint32_t)ip);
+            if (lane == 0) T::put(tab, h, cur);
             __builtin_amdgcn_s_waitcnt(0xc07f);
-            const bool ok_dist = !T::kDistCheck || (int64_t)cand + 65535 >= ip;
-            if (ok_dist && ld32(src + cand) == ld32(src + ip)) {
-                match = cand;
+            const bool ok = cand >= low_idx && (!T::kDistCheck || cand + 65535u >= cur);
+            const int64_t cpos = ok ? (int64_t)cand - (int64_t)ibase : ip;
+            if (ok && ld32(w + cpos) == ld32(w + ip)) {
+                match = cpos;
                 tok_pos = op;
                 if (lane == 0) dst[tok_pos] = 0;
                 op += 1;
@@ -298,7 +339,7 @@ __device__ int64_t compress_block(const uint8_t* __restrict__ src, int64_t n, ui
 
 last_literals:
     {   // lz4.c:1266-1293
-        const int64_t run = n - anchor;
+        const int64_t run = iend - anchor;
         if (limited && op + run + 1 + (run + 255 - 15) / 255 > cap) return 0;
         const int64_t tpos = op;
         op += 1;
@@ -308,10 +349,26 @@ last_literals:
         } else if (lane == 0) {
             dst[tpos] = (uint8_t)(run << 4);
         }
-        wave_copy(dst + op, src + anchor, run, cap - op, n - anchor, lane);
+        wave_copy(dst + op, w + anchor, run, cap - op, iend - anchor, lane);
         op += run;
     }
     return op;
+}
+
+// zero the 16 KiB table (a fresh stream: lz4.c:1513, 1522 / LZ4_prepareTable)
+__device__ __forceinline__ void zero_table(uint16_t* tab, uint32_t lane) {
+    u32x4* t4 = reinterpret_cast<u32x4*>(tab);
+    for (int k = lane; k < 16384 / 16; k += kWave) t4[k] = u32x4{0, 0, 0, 0};
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0)
+}
+
+// One block with a fresh table (LZ4_compress_generic_validated, noDict).
+template <int V>
+__device__ __forceinline__ int64_t compress_block(const uint8_t* __restrict__ src, int64_t n, uint8_t* dst,
+                                                  int64_t cap, int accel, uint16_t* tab, uint32_t lane) {
+    if (n > kMaxInput) return 0;
+    zero_table(tab, lane);
+    return compress_block_w<V>(src, 0, n, dst, cap, accel, tab, lane, 0u, 0u, 0, 0);
 }
 
 template <int V>
@@ -349,6 +406,186 @@ __global__ __launch_bounds__(64) void compress_kernel_auto(const uint8_t* __rest
             r = compress_block<LZ4M_TABLE_U32_HASH5>(src + src_off[b], len, dst + dst_off[b], dst_cap[b], accel,
                                                      tab, lane);
         if (lane == 0) out_len[b] = (int32_t)r;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Blocks with history: lz4.block.compress(dict=) and linked frames.
+// ---------------------------------------------------------------------------
+
+using TabU32 = Table<LZ4M_TABLE_U32_HASH5>;
+constexpr uint32_t kWin = 65536;   // LZ4 window / LZ4_loadDict's index origin
+
+// lz4.block.compress(source, dict=D) (_block.c:93-107): LZ4_resetStream,
+// LZ4_loadDict (lz4.c:1541-1581), LZ4_compress_fast_continue (lz4.c:1684-1701,
+// usingExtDict).  dict_len[b] < 0: no dictionary (a reset stream, as
+// lz4.block.compress without dict=).  Otherwise the last min(D, 64 KiB) bytes
+// of the dictionary sit immediately before the source in `src`.
+__global__ __launch_bounds__(64) void compress_dict_kernel(const uint8_t* __restrict__ src,
+                                                           const int64_t* __restrict__ src_off,
+                                                           const int32_t* __restrict__ src_len,
+                                                           const int32_t* __restrict__ dict_len, uint8_t* dst,
+                                                           const int64_t* __restrict__ dst_off,
+                                                           const int32_t* __restrict__ dst_cap,
+                                                           int32_t* __restrict__ out_len, int64_t n, int accel) {
+    __shared__ __attribute__((aligned(16))) uint16_t tab[8192];
+    uint32_t* t32 = reinterpret_cast<uint32_t*>(tab);
+    const uint32_t lane = threadIdx.x;
+    for (int64_t b = blockIdx.x; b < n; b += gridDim.x) {
+        const int64_t len = src_len[b];
+        const int64_t dl = dict_len[b];
+        const uint8_t* s = src + src_off[b];
+        int64_t r;
+        zero_table(tab, lane);
+        if (dl < 0) {
+            r = compress_block_w<LZ4M_TABLE_U32_HASH5>(s, 0, len, dst + dst_off[b], dst_cap[b], accel, tab, lane,
+                                                       0u, 0u, 0, 0);
+        } else if (dl < 8) {   // no dictionary kept (lz4.c:1564-1566): prefix mode, dictSmall, offset 64 KiB
+            r = compress_block_w<LZ4M_TABLE_U32_HASH5>(s, 0, len, dst + dst_off[b], dst_cap[b], accel, tab, lane,
+                                                       kWin, kWin, 0, 0);
+        } else {
+            const int64_t dt = dl < (int64_t)kWin ? dl : (int64_t)kWin;
+            const uint8_t* w = s - dt;
+            const uint32_t ibase = kWin - (uint32_t)dt;
+            // every third position, later positions win (lz4.c:1575-1578)
+            for (int64_t p = 3 * (int64_t)lane; p <= dt - 8; p += 3 * kWave)
+                atomicMax(&t32[TabU32::hash(w + p)], ibase + (uint32_t)p);
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            r = compress_block_w<LZ4M_TABLE_U32_HASH5>(w, dt, len, dst + dst_off[b], dst_cap[b], accel, tab, lane,
+                                                       ibase, ibase, dt, 0);
+        }
+        if (lane == 0) out_len[b] = (int32_t)r;
+    }
+}
+
+// Linked blocks, serially: one wave per stream (a block with link[b] == 0 and
+// the blocks after it with link == 1), the table carried in LDS from block to
+// block exactly as LZ4_compress_fast_continue carries it (prefix mode over
+// the contiguous source, lz4.c:1665-1675; LZ4F_compressBlock_continue,
+// lz4frame.c:865-871).  The 2 GB renormalisation (LZ4_renormDictT,
+// lz4.c:1612-1630) is applied as a window shift.
+__global__ __launch_bounds__(64) void compress_chain_kernel(const uint8_t* __restrict__ src,
+                                                            const int64_t* __restrict__ src_off,
+                                                            const int32_t* __restrict__ src_len,
+                                                            const int32_t* __restrict__ link, uint8_t* dst,
+                                                            const int64_t* __restrict__ dst_off,
+                                                            const int32_t* __restrict__ dst_cap,
+                                                            int32_t* __restrict__ out_len, int64_t n, int accel) {
+    __shared__ __attribute__((aligned(16))) uint16_t tab[8192];
+    uint32_t* t32 = reinterpret_cast<uint32_t*>(tab);
+    const uint32_t lane = threadIdx.x;
+    for (int64_t b0 = blockIdx.x; b0 < n; b0 += gridDim.x) {
+        if (b0 > 0 && link[b0]) continue;
+        zero_table(tab, lane);
+        const uint8_t* w = src + src_off[b0];
+        uint32_t start = 0;
+        for (int64_t b = b0; b < n && (b == b0 || link[b]); ++b) {
+            const int64_t len = src_len[b];
+            if ((uint64_t)start + (uint64_t)len > 0x80000000ull) {
+                const uint32_t delta = start - kWin;
+                for (int i = lane; i < 4096; i += kWave) {
+                    const uint32_t v = t32[i];
+                    t32[i] = v < delta ? 0u : v - delta;
+                }
+                __builtin_amdgcn_s_waitcnt(0xc07f);
+                w += delta;
+                start = kWin;
+            }
+            const int64_t hist = (src + src_off[b]) - w;
+            const int64_t r = compress_block_w<LZ4M_TABLE_U32_HASH5>(w, hist, len, dst + dst_off[b], dst_cap[b],
+                                                                     accel, tab, lane, 0u, 0u, 0, 0);
+            if (lane == 0) out_len[b] = (int32_t)r;
+            start += (uint32_t)len;
+        }
+    }
+}
+
+// Linked blocks, speculatively in parallel: one wave per block, passes until
+// nothing changes.  A block of a linked stream depends on the stream only
+// through the table its predecessor leaves behind, and only through the
+// entries of the predecessor itself: every older position is more than 65535
+// bytes back when blocks are >= 64 KiB (lz4.c:1062-1065).  Each block runs in
+// its own index space -- its window starts 64 KiB before it, its first byte
+// has index 65536 -- so every table entry older than its predecessor reads as
+// "too far" and a table is handed on by shifting it into the successor's
+// index space (entries that become too far are cleared).
+//   pass 0: every block compresses from an empty table (speculation);
+//   pass j: a block whose predecessor's table changed in pass j-1 compresses
+//           again from that table; the others keep their result.
+// When a pass changes no table, every block's last run used the table its
+// predecessor really leaves, and by induction from the stream's first block
+// (a fresh table) every output equals the serial chain's.
+__global__ __launch_bounds__(64) void compress_spec_kernel(
+    const uint8_t* __restrict__ src, const int64_t* __restrict__ src_off, const int32_t* __restrict__ src_len,
+    const int32_t* __restrict__ link, uint8_t* dst, const int64_t* __restrict__ dst_off,
+    const int32_t* __restrict__ dst_cap, int32_t* __restrict__ out_len, int64_t n, int accel,
+    const uint32_t* __restrict__ t_prev, uint32_t* __restrict__ t_cur, const uint8_t* __restrict__ chg_prev,
+    uint8_t* __restrict__ chg_cur, int32_t* counters, int pass) {
+    __shared__ __attribute__((aligned(16))) uint16_t tab[8192];
+    u32x4* t4 = reinterpret_cast<u32x4*>(tab);
+    const uint32_t lane = threadIdx.x;
+    for (int64_t b = blockIdx.x; b < n; b += gridDim.x) {
+        const bool linked = b > 0 && link[b] != 0;
+        const bool feeds = b + 1 < n && link[b + 1] != 0;   // someone reads this block's table
+        const u32x4* mine_prev = reinterpret_cast<const u32x4*>(t_prev + (size_t)b * 4096);
+        u32x4* mine_cur = reinterpret_cast<u32x4*>(t_cur + (size_t)b * 4096);
+        const bool redo = pass == 0 || (linked && chg_prev[b - 1] != 0);
+        if (!redo) {   // input unchanged: keep output and table
+            if (feeds)
+                for (int k = lane; k < 1024; k += kWave) mine_cur[k] = mine_prev[k];
+            if (lane == 0) chg_cur[b] = 0;
+            continue;
+        }
+        const int64_t len = src_len[b];
+        int64_t hist = 0;
+        if (linked) {
+            if (src_len[b - 1] < (int32_t)kWin) {   // speculation needs >= 64 KiB predecessors
+                if (lane == 0) {
+                    atomicOr(&counters[1], 1);
+                    out_len[b] = 0;
+                    chg_cur[b] = 0;
+                }
+                continue;
+            }
+            hist = kWin;
+        }
+        if (pass == 0 || !linked) {
+            zero_table(tab, lane);
+        } else {
+            const u32x4* pred = reinterpret_cast<const u32x4*>(t_prev + (size_t)(b - 1) * 4096);
+            for (int k = lane; k < 1024; k += kWave) t4[k] = pred[k];
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+        }
+        const uint8_t* w = src + src_off[b] - hist;
+        const int64_t r = compress_block_w<LZ4M_TABLE_U32_HASH5>(w, hist, len, dst + dst_off[b], dst_cap[b],
+                                                                 accel, tab, lane, 0u, 0u, 0, 0);
+        if (lane == 0) out_len[b] = (int32_t)r;
+        if (!feeds) {
+            if (lane == 0) chg_cur[b] = 0;
+            continue;
+        }
+        // hand the table on in the successor's index space: index i here is
+        // index i - shift there; entries the successor can never use become 0
+        const uint32_t shift = (uint32_t)(len + hist) - kWin;
+        bool diff = false;
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        for (int k = lane; k < 1024; k += kWave) {
+            u32x4 v = t4[k];
+            v.x = v.x > shift ? v.x - shift : 0u;
+            v.y = v.y > shift ? v.y - shift : 0u;
+            v.z = v.z > shift ? v.z - shift : 0u;
+            v.w = v.w > shift ? v.w - shift : 0u;
+            mine_cur[k] = v;
+            if (pass != 0) {
+                const u32x4 o = mine_prev[k];
+                diff |= (o.x != v.x) | (o.y != v.y) | (o.z != v.z) | (o.w != v.w);
+            }
+        }
+        const bool changed = pass == 0 || __ballot(diff) != 0;
+        if (lane == 0) {
+            chg_cur[b] = changed ? 1 : 0;
+            if (changed) atomicAdd(&counters[0], 1);
+        }
     }
 }
 
@@ -394,4 +631,67 @@ extern "C" int lz4m_compress_batch(const uint8_t* d_src, const int64_t* d_src_of
             return LZ4M_EINVAL;
     }
     return (int)hipGetLastError();
+}
+
+extern "C" int lz4m_compress_dict_batch(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len,
+                                        const int32_t* d_dict_len, uint8_t* d_dst, const int64_t* d_dst_off,
+                                        const int32_t* d_dst_cap, int32_t* d_out_len, int64_t n, int acceleration,
+                                        lz4m_stream_t stream) {
+    if (n < 0) return LZ4M_EINVAL;
+    if (n == 0) return 0;
+    if (acceleration < 1) acceleration = 1;
+    if (acceleration > 65537) acceleration = 65537;
+    const uint32_t grid = (uint32_t)(n < (1ll << 30) ? n : (1ll << 30));
+    hipLaunchKernelGGL(compress_dict_kernel, dim3(grid), dim3(64), 0, (hipStream_t)stream, d_src, d_src_off,
+                       d_src_len, d_dict_len, d_dst, d_dst_off, d_dst_cap, d_out_len, n, acceleration);
+    return (int)hipGetLastError();
+}
+
+static thread_local int g_linked_passes = 0;
+extern "C" int lz4m_compress_linked_passes(void) { return g_linked_passes; }
+
+extern "C" size_t lz4m_compress_linked_workspace_size(int64_t n) {
+    if (n <= 0) return 64;
+    return 64 + (size_t)n * 2 * 16384 + (((size_t)n * 2 + 63) & ~(size_t)63);
+}
+
+extern "C" int lz4m_compress_linked_batch(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len,
+                                          const int32_t* d_link, uint8_t* d_dst, const int64_t* d_dst_off,
+                                          const int32_t* d_dst_cap, int32_t* d_out_len, int64_t n, int acceleration,
+                                          int mode, void* d_work, size_t work_bytes, lz4m_stream_t stream) {
+    if (n < 0 || (mode != LZ4M_LINKED_SERIAL && mode != LZ4M_LINKED_SPECULATIVE)) return LZ4M_EINVAL;
+    if (n == 0) return 0;
+    if (acceleration < 1) acceleration = 1;
+    if (acceleration > 65537) acceleration = 65537;
+    hipStream_t s = (hipStream_t)stream;
+    const uint32_t grid = (uint32_t)(n < (1ll << 30) ? n : (1ll << 30));
+    if (mode == LZ4M_LINKED_SERIAL) {
+        hipLaunchKernelGGL(compress_chain_kernel, dim3(grid), dim3(64), 0, s, d_src, d_src_off, d_src_len, d_link,
+                           d_dst, d_dst_off, d_dst_cap, d_out_len, n, acceleration);
+        return (int)hipGetLastError();
+    }
+    if (d_work == nullptr || work_bytes < lz4m_compress_linked_workspace_size(n)) return LZ4M_EINVAL;
+    uint8_t* base = (uint8_t*)d_work;
+    int32_t* counters = (int32_t*)base;
+    uint32_t* tb[2] = {(uint32_t*)(base + 64), (uint32_t*)(base + 64 + (size_t)n * 16384)};
+    uint8_t* cb[2] = {base + 64 + (size_t)n * 32768, base + 64 + (size_t)n * 32768 + (size_t)n};
+    int32_t h_counters[2] = {0, 0};
+    g_linked_passes = 0;
+    for (int64_t pass = 0; pass <= n; ++pass) {
+        g_linked_passes = (int)pass + 1;
+        hipError_t e = hipMemsetAsync(counters, 0, 8, s);
+        if (e != hipSuccess) return (int)e;
+        const int cur = (int)(pass & 1), prev = cur ^ 1;
+        hipLaunchKernelGGL(compress_spec_kernel, dim3(grid), dim3(64), 0, s, d_src, d_src_off, d_src_len, d_link,
+                           d_dst, d_dst_off, d_dst_cap, d_out_len, n, acceleration, tb[prev], tb[cur], cb[prev],
+                           cb[cur], counters, (int)pass);
+        e = hipGetLastError();
+        if (e != hipSuccess) return (int)e;
+        e = hipMemcpyAsync(h_counters, counters, 8, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) return (int)e;
+        if (h_counters[1]) return LZ4M_EINVAL;
+        if (h_counters[0] == 0) return 0;
+    }
+    return 0;
 }

@@ -26,6 +26,8 @@ TABLE_AUTO = 2
 PARSE_PARALLEL = 3   # parallel-parse compressor: valid blocks, ratio of LZ4_compress_default
 PARSE_PARALLEL_LARGE = 4   # the same for blocks > 64 KiB
 PARSE_PARALLEL_HQ = 5   # PARSE_PARALLEL with the reference's 13-bit table (ratio of LZ4_compress_default)
+LINKED_SERIAL = 1        # lz4m_compress_linked_batch modes
+LINKED_SPECULATIVE = 2
 EINVAL = 0x10000
 # decoder selector of lz4m_decompress_batch_sel (include/lz4m.h)
 DECODERS = {"auto": 0, "lane": 1, "coop": 2, "hist": 3, "rows": 4, "direct": 5}
@@ -48,6 +50,10 @@ def _declare(lib) -> None:
         "lz4m_decompress_batch_dict": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, vp], i32),
         "lz4m_decompress_chain": ([vp, vp, vp, vp, vp, vp, i64, i32, vp], i32),
         "lz4m_compress_batch": ([vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, vp], i32),
+        "lz4m_compress_dict_batch": ([vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, vp], i32),
+        "lz4m_compress_linked_workspace_size": ([i64], C.c_size_t),
+        "lz4m_compress_linked_passes": ([], i32),
+        "lz4m_compress_linked_batch": ([vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, vp, C.c_size_t, vp], i32),
         "lz4m_xxh32_batch": ([vp, vp, vp, u32, vp, i64, vp], i32),
         "lz4m_xxh32_long": ([vp, i64, u32, vp, vp], i32),
         "lz4m_scan_scratch_entries": ([i64], i64),
@@ -167,6 +173,28 @@ def launch_compress(src, src_off, src_len, dst, dst_off, dst_cap, out_len, n, ta
     rc = lib().lz4m_compress_batch(ptr(src), ptr(src_off), ptr(src_len), ptr(dst), ptr(dst_off), ptr(dst_cap),
                                    ptr(out_len), n, table, accel, stream_ptr(stream))
     check(rc, "lz4m_compress_batch")
+
+
+def launch_compress_dict(src, src_off, src_len, dict_len, dst, dst_off, dst_cap, out_len, n, accel,
+                         stream=None) -> None:
+    """lz4.block.compress(dict=) per block; the dictionary tail precedes each block in ``src``."""
+    rc = lib().lz4m_compress_dict_batch(ptr(src), ptr(src_off), ptr(src_len), ptr(dict_len), ptr(dst), ptr(dst_off),
+                                        ptr(dst_cap), ptr(out_len), n, accel, stream_ptr(stream))
+    check(rc, "lz4m_compress_dict_batch")
+
+
+def launch_compress_linked(src, src_off, src_len, link, dst, dst_off, dst_cap, out_len, n, accel,
+                           mode: int = LINKED_SPECULATIVE, stream=None) -> None:
+    """Linked-block streams (lz4m_compress_linked_batch).  The speculative
+    mode synchronises ``stream`` once per pass."""
+    L = lib()
+    work = None
+    if mode == LINKED_SPECULATIVE:
+        work = torch.empty(int(L.lz4m_compress_linked_workspace_size(n)), dtype=torch.uint8, device=src.device)
+    rc = L.lz4m_compress_linked_batch(ptr(src), ptr(src_off), ptr(src_len), ptr(link), ptr(dst), ptr(dst_off),
+                                      ptr(dst_cap), ptr(out_len), n, accel, mode, ptr(work),
+                                      0 if work is None else work.numel(), stream_ptr(stream))
+    check(rc, "lz4m_compress_linked_batch")
 
 
 def launch_xxh32_batch(src, off, length, seed, out, n, stream=None) -> None:

@@ -88,21 +88,23 @@ def compress(source, mode="default", store_size=True, acceleration=1, compressio
     Compress source into one LZ4 block (``_block.c:127-271``), output
     byte-identical to the reference: ``lz4.block.compress`` resets an
     ``LZ4_stream_t`` and calls ``LZ4_compress_fast_continue`` (byU32 table,
-    hash5), which ``TABLE_U32_HASH5`` reproduces.
+    hash5), which ``TABLE_U32_HASH5`` reproduces.  With ``dict`` (any
+    length, even empty) the stream is first loaded with ``LZ4_loadDict``
+    (``_block.c:101-104``, ``lz4.c:1541-1581``) -- lz4m_compress_dict_batch.
     """
     src = _buffer(source)
     acceleration = _c_int(acceleration, "acceleration")
     _c_int(compression, "compression")
     if src.nbytes > INT_MAX:
         raise OverflowError("Input too large for LZ4 API")
+    d = None
     if dict is not None:
         d = _buffer(dict, "dict")
         if d.nbytes > INT_MAX:
             raise OverflowError("Dictionary too large for LZ4 API")
-        if d.nbytes:
-            raise NotImplementedError("compress(dict=...) is not provided by the MI355X codec yet")
     accel = _mode_accel(mode, acceleration)
-    out = compress_many([src], accel=accel, store_size=bool(store_size), as_bytearray=bool(return_bytearray))[0]
+    out = compress_many([src], accel=accel, store_size=bool(store_size), as_bytearray=bool(return_bytearray),
+                        dict=d)[0]
     if out is None:
         raise LZ4BlockError("Compression failed")
     return out
@@ -184,9 +186,11 @@ class _Layout:
 
 def _stage_in(dev, views, offs, lens, d_off, caps, skip=None):
     """Stage tables + packed payload, copy them to the device in one go;
-    returns (layout, host, device) with the device views ready to launch on."""
-    n = len(views)
-    payload = sum(lens)
+    returns (layout, host, device) with the device views ready to launch on.
+    ``views`` are packed back to back; ``offs``/``lens`` (one per block) say
+    where the blocks are in that payload."""
+    n = len(offs)
+    payload = sum(v.nbytes for v in views)
     lay = _Layout(n, payload, sum(caps))
     h, d = _stage(dev, lay.total, lay.total)
     hn = h.numpy()
@@ -219,22 +223,37 @@ def _stage_out(lay: _Layout, h: torch.Tensor, d: torch.Tensor, n: int):
 
 
 def compress_many(blocks, accel: int = 1, store_size: bool = True, as_bytearray: bool = False,
-                  table: int = N.TABLE_U32_HASH5):
+                  table: int = N.TABLE_U32_HASH5, dict=None):
     """Compress a sequence of host buffers as independent blocks in one
     launch.  Returns a list of bytes (None for a block that failed, i.e.
-    input larger than LZ4_MAX_INPUT_SIZE)."""
+    input larger than LZ4_MAX_INPUT_SIZE).  ``dict`` (a buffer, possibly
+    empty): every block is compressed as lz4.block.compress(dict=dict) does;
+    the dictionary's last 64 KiB are staged in front of each block."""
     views = [_buffer(b) for b in blocks]
     dev = N.device()
     n = len(views)
     if n == 0:
         return []
     lens = [v.nbytes for v in views]
-    offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.int64)]) if n > 1 else np.zeros(1, np.int64)
     caps = [max(N.compress_bound(L), 1) for L in lens]
     d_off = np.concatenate([[0], np.cumsum(caps[:-1], dtype=np.int64)]) if n > 1 else np.zeros(1, np.int64)
-    lay, h, d = _stage_in(dev, views, offs, lens, d_off, caps)
+    if dict is None:
+        offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.int64)]) if n > 1 else np.zeros(1, np.int64)
+        payload = views
+    else:
+        dv = _buffer(dict, "dict")
+        tail = dv[-65536:] if dv.nbytes >= 8 else dv[:0]   # LZ4_loadDict keeps the last 64 KiB (lz4.c:1568)
+        t = tail.nbytes
+        offs = np.arange(1, n + 1, dtype=np.int64) * t + (np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.int64)])
+                                                            if n > 1 else np.zeros(1, np.int64))
+        payload = [x for v in views for x in (tail, v)]
+    lay, h, d = _stage_in(dev, payload, offs, lens, d_off, caps)
     d_src, src_off, src_len, d_dst, dst_off, dst_cap, out_len = _dev_views(lay, d, n)
-    N.launch_compress(d_src, src_off, src_len, d_dst, dst_off, dst_cap, out_len, n, table, accel)
+    if dict is None:
+        N.launch_compress(d_src, src_off, src_len, d_dst, dst_off, dst_cap, out_len, n, table, accel)
+    else:
+        dict_len = torch.full((n,), dv.nbytes, dtype=torch.int32, device=dev)
+        N.launch_compress_dict(d_src, src_off, src_len, dict_len, d_dst, dst_off, dst_cap, out_len, n, accel)
     olen, host = _stage_out(lay, h, d, n)
     res = []
     for i in range(n):

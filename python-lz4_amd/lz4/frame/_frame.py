@@ -6,9 +6,12 @@ get_frame_info 640-824, __decompress 938-1193) over the frame format of
 LE32 block records); every byte-level operation runs on the GPU:
 
 * compress: the input is cut into blocks and compressed in one batched
-  launch with the LZ4_compress_fast_extState_fastReset parse
-  (lz4frame.c:853-863 -> lz4.c:1378-1413, cap = block size - 1, raw block when
-  it does not fit, lz4frame.c:834-842); block records are emitted by
+  launch (cap = block size - 1, raw block when it does not fit,
+  lz4frame.c:834-842) -- independent blocks with the
+  LZ4_compress_fast_extState_fastReset parse (lz4frame.c:853-863 ->
+  lz4.c:1378-1413), linked blocks (the default) as one
+  LZ4_compress_fast_continue stream (lz4frame.c:865-871), speculatively in
+  parallel (lz4m_compress_linked_batch); block records are emitted by
   ``lz4m_frame_emit`` at scanned offsets.  The content checksum (XXH32 over
   all input, lz4frame.c:1042, 1171) is one serial stream: it runs on a host
   core (lz4m_xxh32_host_*) in a thread beside the device work -- on the
@@ -20,11 +23,10 @@ LE32 block records); every byte-level operation runs on the GPU:
   verified on the device, the content checksum on a host core.  Linked-block frames decode
   block after block on one wavefront with the previous output as prefix.
 
-Scope notes: ``block_linked=True`` frames are written with the
-linked flag but independently compressed blocks -- a valid frame that every
-decoder accepts, a little larger than the reference's at 64 KiB blocks; HC
-levels (>= 3) and the chunked / context streaming API are outside this
-codec's scope.
+Scope notes: every frame ``compress`` writes is byte-identical
+to the reference's (``parse="parallel"`` on ``compress_device`` trades that
+for speed); HC levels (>= 3) and the chunked / context streaming API are
+outside this codec's scope.
 """
 from __future__ import annotations
 
@@ -97,6 +99,11 @@ class _HashThread(threading.Thread):
 
 
 # ------------------------------------------------------------------ header
+# linked frames with at least this many blocks compress speculatively in
+# parallel (lz4m_compress_linked_batch); shorter ones one wavefront per frame
+_SPEC_MIN_BLOCKS = int(os.environ.get("LZ4M_SPEC_MIN_BLOCKS", "4"))
+
+
 def _optimal_bsid(requested: int, size: int) -> int:
     """LZ4F_optimalBSID (lz4frame.c:351-363)."""
     proposed, max_size = 4, 64 << 10
@@ -267,11 +274,18 @@ def _compress_frame(d_src, n=None, *, compression_level=0, block_size=0, content
         cmp = torch.empty(nb * slot, dtype=torch.uint8, device=dev)
         cmp_off = torch.arange(nb, dtype=torch.int64, device=dev) * slot
         cmp_len = torch.empty(nb, dtype=torch.int32, device=dev)
-        if parse == "exact":
-            table = N.TABLE_AUTO
+        if parse == "exact" and linked:   # one stream across the blocks (lz4frame.c:865-871)
+            link = torch.ones(nb, dtype=torch.int32, device=dev)
+            link[0] = 0
+            mode = N.LINKED_SPECULATIVE if nb >= _SPEC_MIN_BLOCKS else N.LINKED_SERIAL
+            N.launch_compress_linked(d_src, raw_off, raw_len, link, cmp, cmp_off, cap, cmp_len, nb, accel,
+                                     mode=mode, stream=stream)
         else:
-            table = N.PARSE_PARALLEL if bsize <= 65536 else N.PARSE_PARALLEL_LARGE
-        N.launch_compress(d_src, raw_off, raw_len, cmp, cmp_off, cap, cmp_len, nb, table, accel, stream)
+            if parse == "exact":
+                table = N.TABLE_AUTO
+            else:
+                table = N.PARSE_PARALLEL if bsize <= 65536 else N.PARSE_PARALLEL_LARGE
+            N.launch_compress(d_src, raw_off, raw_len, cmp, cmp_off, cap, cmp_len, nb, table, accel, stream)
         rec_len = torch.empty(nb, dtype=torch.int32, device=dev)
         N.frame_block_sizes(raw_len, cmp_len, block_checksum, rec_len, nb, stream)
         frame_off = N.exclusive_scan(rec_len, stream=stream)

@@ -8,7 +8,10 @@ records inputs and the reference's outputs:
   * LZ4_decompress_safe status (size or -(pos)-1) for valid and malformed
     blocks (mutations, truncations, capacities);
   * XXH32 of every input for several seeds;
-  * LZ4F_compressFrame frames for several preference sets;
+  * LZ4F_compressFrame frames for several preference sets (independent and
+    linked blocks);
+  * lz4.block.compress(dict=) outputs (LZ4_resetStream + LZ4_loadDict +
+    LZ4_compress_fast_continue, _block.c:93-107) for dictionaries of 0..100000 B;
   * the reference tests' own data file tests/block/numpy_byte_array.bin and
     the known-answer vectors of tests/block/test_block_1.py:128-149.
 Vectors are data only; nothing of the reference's source is stored.
@@ -35,7 +38,7 @@ def main():
     ref = O.Reference()
     rng = random.Random(20261015)
     arrays, man = {}, {"version": ref.version(), "inputs": [], "compress": [], "decompress": [],
-                       "xxh32": [], "frames": [], "kat": []}
+                       "xxh32": [], "frames": [], "kat": [], "dict_compress": []}
 
     def add(name, data):
         arrays[name] = np.frombuffer(bytes(data), dtype=np.uint8)
@@ -115,6 +118,31 @@ def main():
                  dict(block_size_id=4, linked=False, level=-3)]:
         fr = ref.compress_frame(fdata, **opts)
         man["frames"].append({"input": "text_300k", "opts": opts, "key": add(f"fr_{len(man['frames'])}", fr)})
+
+    # more linked frames: ~513 KiB of mixed data, several block sizes / levels
+    parts = {k: _synth.blocks(3, k, seed=41).tobytes() for k in ("silesia", "runs", "random", "text")}
+    mixed = (parts["silesia"][:196608] + parts["random"][:65536] + parts["runs"][:65536]
+             + parts["text"][:196608] + parts["random"][65536:65536 + 1000])   # a raw block mid-stream
+    add("in_mixed_1m", mixed)
+    man["inputs"].append({"name": "mixed_1m", "key": "in_mixed_1m", "len": len(mixed)})
+    for opts in [dict(block_size_id=4, linked=True, content_checksum=True),
+                 dict(block_size_id=4, linked=True, content_checksum=False, block_checksum=True, level=-2),
+                 dict(block_size_id=5, linked=True, content_checksum=True)]:
+        fr = ref.compress_frame(mixed, **opts)
+        man["frames"].append({"input": "mixed_1m", "opts": opts, "key": add(f"fr_{len(man['frames'])}", fr)})
+
+    # lz4.block.compress(dict=)
+    dsrc = _synth.blocks(4, "text", seed=77).tobytes() + _synth.blocks(2, "records", seed=78).tobytes()
+    dcases = [("text_64k", 0, 1), ("text_64k", 5, 1), ("text_64k", 8, 1), ("text_64k", 100, 1),
+              ("text_64k", 20000, 1), ("text_64k", 65536, 1), ("text_64k", 100000, 1), ("text_64k", 20000, 3),
+              ("records_ragged", 30000, 1), ("numpy_byte_array", 4096, 1), ("text_len13", 50, 1),
+              ("text_len0", 1000, 1), ("text_300k", 65536, 2), ("zeros_64k", 300, 1)]
+    for i, (name, dl, acc) in enumerate(dcases):
+        data = dict(inputs)[name]
+        dd = dsrc[len(dsrc) - dl:] if dl else b""
+        c = ref.compress_dict(data, dd, acc)
+        man["dict_compress"].append({"input": name, "dict": add(f"dict_{i}", dd), "accel": acc,
+                                     "key": add(f"cdict_{i}", c)})
 
     np.savez_compressed(os.path.join(HERE, "golden.npz"), **arrays)
     with open(os.path.join(HERE, "manifest.json"), "w") as f:

@@ -64,6 +64,17 @@ def test_argument_validation_without_gpu():
     assert lib.lz4m_decompress_batch(None, None, None, None, None, None, None, -1, None) == N.EINVAL
     assert lib.lz4m_compress_batch(None, None, None, None, None, None, None, 0, 0, 1, None) == 0
     assert lib.lz4m_compress_batch(None, None, None, None, None, None, None, -5, 0, 1, None) == N.EINVAL
+    assert lib.lz4m_compress_dict_batch(None, None, None, None, None, None, None, None, 0, 1, None) == 0
+    assert lib.lz4m_compress_dict_batch(None, None, None, None, None, None, None, None, -1, 1, None) == N.EINVAL
+    for mode in (N.LINKED_SERIAL, N.LINKED_SPECULATIVE):
+        assert lib.lz4m_compress_linked_batch(None, None, None, None, None, None, None, None, 0, 1, mode,
+                                              None, 0, None) == 0
+    assert lib.lz4m_compress_linked_batch(None, None, None, None, None, None, None, None, 4, 1, 7,
+                                          None, 0, None) == N.EINVAL
+    # speculative mode without enough scratch is refused before any launch
+    assert lib.lz4m_compress_linked_batch(None, None, None, None, None, None, None, None, 4, 1,
+                                          N.LINKED_SPECULATIVE, None, 0, None) == N.EINVAL
+    assert lib.lz4m_compress_linked_workspace_size(4) >= 4 * 2 * 16384
     assert lib.lz4m_xxh32_batch(None, None, None, 0, None, -1, None) == N.EINVAL
     assert lib.lz4m_xxh32_long(None, -1, 0, None, None) == N.EINVAL
     assert lib.lz4m_frame_scan(None, -1, 0, 0, 0, 65536, 1, None, None, None, None, None) == N.EINVAL

@@ -151,6 +151,38 @@ def test_block_dict_decompress(gpu, reference):
         lz4.block.decompress(comp, uncompressed_size=len(x))
 
 
+def test_block_dict_compress_golden(gpu, golden):
+    """lz4.block.compress(dict=) is byte-identical to the reference
+    (LZ4_loadDict + LZ4_compress_fast_continue, _block.c:101-104)."""
+    man, arr = golden
+    inputs = {e["name"]: _b(arr, e["key"]) for e in man["inputs"]}
+    for e in man["dict_compress"]:
+        data, d = inputs[e["input"]], _b(arr, e["dict"])
+        mode = ("default", 1) if e["accel"] == 1 else ("fast", e["accel"])
+        got = lz4.block.compress(data, mode=mode[0], acceleration=mode[1], store_size=False, dict=d)
+        assert got == _b(arr, e["key"]), e
+        assert lz4.block.decompress(got, uncompressed_size=len(data), dict=d) == data
+
+
+def test_block_dict_compress_vs_oracle(gpu, oracle):
+    """Batched dict= compression over dictionary lengths around every
+    LZ4_loadDict boundary, against the CPU restatement."""
+    from lz4 import _synth
+    import random
+    rng = random.Random(3)
+    for kind in ("text", "records", "random", "runs", "silesia"):
+        blob = _synth.blocks(4, kind, seed=22).tobytes()
+        for dl in (0, 3, 7, 8, 9, 64, 5000, 65535, 65536, 65537, 131072):
+            d = blob[:dl]
+            srcs = []
+            for sl in (0, 12, 13, 777, 65536, 70000):
+                o = rng.randrange(dl, len(blob) - sl + 1)
+                srcs.append(blob[o:o + sl])
+            got = lz4.block.compress_many(srcs, store_size=False, dict=d)
+            for sv, g in zip(srcs, got):
+                assert g == oracle.compress_dict(sv, d), (kind, dl, len(sv))
+
+
 def test_many_matches_single(gpu):
     from lz4 import _synth
     blocks = [b.tobytes() for b in _synth.blocks(32, "silesia", seed=1)]
@@ -189,20 +221,108 @@ def test_frame_roundtrip(gpu, data, block_size, block_linked, checksums, store_s
     assert d == bytes(data) and nread == len(c)
 
 
-def test_frame_independent_is_reference_bytes(gpu, golden, reference):
-    """Independent-block frames are byte-identical to LZ4F_compressFrame."""
+@pytest.mark.parametrize("spec_min", [2, 1 << 30], ids=["speculative", "serial"])
+def test_frame_is_reference_bytes(gpu, golden, monkeypatch, spec_min):
+    """Independent- and linked-block frames are byte-identical to
+    LZ4F_compressFrame (golden frames of the reference)."""
+    import lz4.frame._frame as F
+    monkeypatch.setattr(F, "_SPEC_MIN_BLOCKS", spec_min)
     man, arr = golden
     inputs = {e["name"]: _b(arr, e["key"]) for e in man["inputs"]}
+    nlinked = 0
     for e in man["frames"]:
         o = e["opts"]
-        if o.get("linked"):
-            continue
+        nlinked += bool(o.get("linked"))
         data = inputs[e["input"]]
-        got = lz4.frame.compress(data, block_size=o["block_size_id"], block_linked=False,
+        got = lz4.frame.compress(data, block_size=o["block_size_id"], block_linked=bool(o.get("linked")),
                                  content_checksum=o.get("content_checksum", True),
                                  block_checksum=o.get("block_checksum", False),
                                  store_size=o.get("store_size", True), compression_level=o.get("level", 0))
         assert got == _b(arr, e["key"]), o
+    assert nlinked >= 4
+
+
+def _linked_case(gpu, data: bytes, bsize: int, accel: int, mode: int):
+    import torch
+    import lz4._native as N
+    n = len(data)
+    nb = (n + bsize - 1) // bsize
+    d = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(gpu)
+    off = torch.arange(nb, dtype=torch.int64, device=gpu) * bsize
+    ln = torch.full((nb,), bsize, dtype=torch.int32, device=gpu)
+    ln[-1] = n - (nb - 1) * bsize
+    link = torch.ones(nb, dtype=torch.int32, device=gpu)
+    link[0] = 0
+    slot = N.compress_bound(bsize)
+    out = torch.zeros(nb * slot, dtype=torch.uint8, device=gpu)
+    oo = torch.arange(nb, dtype=torch.int64, device=gpu) * slot
+    olen = torch.zeros(nb, dtype=torch.int32, device=gpu)
+    N.launch_compress_linked(d, off, ln, link, out, oo, ln - 1, olen, nb, accel, mode=mode)
+    torch.cuda.synchronize()
+    h, ol = out.cpu().numpy(), olen.cpu().tolist()
+    return [h[k * slot: k * slot + ol[k]].tobytes() if ol[k] > 0 else None for k in range(nb)]
+
+
+@pytest.mark.parametrize("mode", ["serial", "speculative"])
+def test_linked_blocks_vs_oracle(gpu, oracle, mode):
+    """Linked streams of every kind and block size, both modes, against
+    orc_compress_linked (pinned to the reference's linked frames)."""
+    import lz4._native as N
+    from lz4 import _synth
+    m = N.LINKED_SERIAL if mode == "serial" else N.LINKED_SPECULATIVE
+    for kind in ("silesia", "text", "records", "runs", "random", "markup"):
+        blob = _synth.blocks(48, kind, seed=5).tobytes()
+        for bsize, n, accel in ((65536, len(blob), 1), (65536, 1_000_003, 3), (262144, len(blob), 1),
+                                (1 << 20, len(blob), 1)):
+            got = _linked_case(gpu, blob[:n], bsize, accel, m)
+            assert got == oracle.compress_linked(blob[:n], bsize, accel), (kind, bsize, n, accel)
+
+
+def test_linked_mixed_streams(gpu, oracle):
+    """Several streams in one batch (serial mode): a block with link 0
+    restarts from a fresh table."""
+    import torch
+    import lz4._native as N
+    from lz4 import _synth
+    blob = _synth.blocks(12, "silesia", seed=6).tobytes()
+    cuts = [0, 70000, 70013, 300000, 300001, 500000, len(blob)]
+    heads = {0, 300001}   # stream 0 has a 13-byte block in the middle
+    d = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(gpu)
+    nb = len(cuts) - 1
+    off = torch.tensor(cuts[:-1], dtype=torch.int64, device=gpu)
+    ln = torch.tensor([cuts[i + 1] - cuts[i] for i in range(nb)], dtype=torch.int32, device=gpu)
+    link = torch.tensor([0 if c in heads else 1 for c in cuts[:-1]], dtype=torch.int32, device=gpu)
+    slot = N.compress_bound(max(ln.tolist()))
+    out = torch.zeros(nb * slot, dtype=torch.uint8, device=gpu)
+    oo = torch.arange(nb, dtype=torch.int64, device=gpu) * slot
+    cap = torch.full((nb,), slot, dtype=torch.int32, device=gpu)
+    olen = torch.zeros(nb, dtype=torch.int32, device=gpu)
+    N.launch_compress_linked(d, off, ln, link, out, oo, cap, olen, nb, 1, mode=N.LINKED_SERIAL)
+    torch.cuda.synchronize()
+    h, ol = out.cpu().numpy(), olen.cpu().tolist()
+    # expected: each stream is a linked chain whose blocks are these cuts
+    k = 0
+    while k < nb:
+        j = k + 1
+        while j < nb and cuts[j] not in heads:
+            j += 1
+        stream = blob[cuts[k]:cuts[j]]
+        # orc_compress_linked uses equal block sizes; restate with the window form per block
+        import ctypes as C
+        tab = (C.c_uint32 * 4096)()
+        for b in range(k, j):
+            blen = cuts[b + 1] - cuts[b]
+            dst = (C.c_uint8 * slot)()
+            buf = np.frombuffer(stream, dtype=np.uint8)
+            oracle.lib.orc_compress_window.argtypes = [C.c_void_p, C.c_int64, C.c_int, C.c_void_p, C.c_int,
+                                                       C.c_int, C.c_void_p, C.c_uint32, C.c_uint32, C.c_int64,
+                                                       C.c_int64]
+            r = oracle.lib.orc_compress_window(buf.ctypes.data_as(C.c_void_p), cuts[b] - cuts[k], blen, dst, slot,
+                                               1, tab, 0, 0, 0, 0)
+            assert ol[b] == r and h[b * slot: b * slot + r].tobytes() == bytes(dst)[:r], b
+        k = j
+    with pytest.raises(RuntimeError):   # speculation needs >= 64 KiB predecessors
+        N.launch_compress_linked(d, off, ln, link, out, oo, cap, olen, nb, 1, mode=N.LINKED_SPECULATIVE)
 
 
 def test_frame_decodes_reference_frames(gpu, golden):

@@ -124,6 +124,71 @@ def test_frame_fixtures_decode_with_oracle(oracle, golden):
             assert struct.unpack_from("<I", fr, len(fr) - 4)[0] == oracle.xxh32(out)
 
 
+def _frame_blocks(fr: bytes):
+    """(block size, linked, [(raw, payload)]) of a frame, by the host scanner."""
+    from lz4.frame._frame import _BLOCK_SIZES, _scan_blocks
+    fr = memoryview(fr)
+    flg, bd = fr[4], fr[5]
+    hsize = 7 + (8 if flg & 8 else 0)
+    info = {"block_checksum": bool(flg & 0x10), "content_checksum": bool(flg & 4),
+            "block_size": _BLOCK_SIZES[(bd >> 4) & 7], "block_linked": not (flg & 0x20)}
+    recs, state = _scan_blocks(fr, hsize, info)
+    assert state[0] == "end"
+    return info["block_size"], info["block_linked"], [(raw, bytes(fr[pos:pos + size])) for raw, pos, size, _ in recs]
+
+
+def test_linked_frames_golden(oracle, golden):
+    """orc_compress_linked reproduces every block of the reference's linked
+    frames (LZ4F_compressBlock_continue, lz4frame.c:865-871)."""
+    man, arr = golden
+    inputs = {e["name"]: _b(arr, e["key"]) for e in man["inputs"]}
+    n = 0
+    for e in man["frames"]:
+        o = e["opts"]
+        if not o.get("linked"):
+            continue
+        bsize, linked, recs = _frame_blocks(_b(arr, e["key"]))
+        assert linked
+        lvl = o.get("level", 0)
+        got = oracle.compress_linked(inputs[e["input"]], bsize, -lvl + 1 if lvl < 0 else 1)
+        assert len(got) == len(recs)
+        for g, (raw, payload) in zip(got, recs):
+            assert (g is None) == raw
+            if not raw:
+                assert g == payload
+        n += 1
+    assert n >= 4
+
+
+def test_dict_compress_golden(oracle, golden):
+    """orc_compress_dict reproduces lz4.block.compress(dict=) (_block.c:101-104)."""
+    man, arr = golden
+    inputs = {e["name"]: _b(arr, e["key"]) for e in man["inputs"]}
+    assert len(man["dict_compress"]) >= 10
+    for e in man["dict_compress"]:
+        got = oracle.compress_dict(inputs[e["input"]], _b(arr, e["dict"]), e["accel"])
+        assert got == _b(arr, e["key"]), e
+
+
+def test_dict_and_linked_vs_reference(oracle, reference):
+    """Differential: dictionary lengths around every LZ4_loadDict boundary
+    (< 8, 64 KiB, > 64 KiB) and linked frames of every block size."""
+    from lz4 import _synth
+    rng = random.Random(12)
+    for kind in ("text", "records", "random", "runs"):
+        blob = _synth.blocks(4, kind, seed=21).tobytes()
+        for dl in (0, 3, 7, 8, 9, 64, 5000, 65535, 65536, 65537, 131072):
+            for sl in (0, 12, 13, 777, 65536, 70000):
+                o = rng.randrange(0, len(blob) - sl - dl + 1)
+                d, s = blob[o:o + dl], blob[o + dl:o + dl + sl]
+                assert oracle.compress_dict(s, d) == reference.compress_dict(s, d), (kind, dl, sl)
+        for bsid, bs in ((4, 65536), (5, 262144)):
+            fr = reference.compress_frame(blob, block_size_id=bsid, linked=True, content_checksum=False)
+            _, _, recs = _frame_blocks(fr)
+            got = oracle.compress_linked(blob, bs)
+            assert [g for g in got] == [None if raw else p for raw, p in recs], (kind, bs)
+
+
 def test_optimal_bsid():
     from lz4.frame._frame import _optimal_bsid
     assert _optimal_bsid(0, 10) == 0

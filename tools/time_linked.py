@@ -1,0 +1,42 @@
+"""Time linked-block compression (serial vs speculative) on device data.
+usage: python tools/time_linked.py [MiB] [kinds...]"""
+import sys, time
+sys.path.insert(0, "python-lz4_amd")
+import torch
+import lz4._native as N
+from lz4 import _synth
+
+mib = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+kinds = sys.argv[2:] or ["silesia"]
+dev = torch.device("cuda", 0)
+L = N.lib()
+for kind in kinds:
+    data = _synth.blocks(mib * 16, kind, seed=3)
+    d = torch.from_numpy(data.reshape(-1)).to(dev)
+    n = d.numel()
+    for bsize in (65536, 4 << 20):
+        nb = (n + bsize - 1) // bsize
+        off = torch.arange(nb, dtype=torch.int64, device=dev) * bsize
+        ln = torch.full((nb,), bsize, dtype=torch.int32, device=dev)
+        ln[-1] = n - (nb - 1) * bsize
+        link = torch.ones(nb, dtype=torch.int32, device=dev)
+        link[0] = 0
+        slot = N.compress_bound(bsize)
+        out = torch.empty(nb * slot, dtype=torch.uint8, device=dev)
+        oo = torch.arange(nb, dtype=torch.int64, device=dev) * slot
+        olen = torch.empty(nb, dtype=torch.int32, device=dev)
+        res = {}
+        for mode, name in ((N.LINKED_SPECULATIVE, "spec"), (N.LINKED_SERIAL, "serial")):
+            if name == "serial" and nb > 64 and mib > 16:
+                continue
+            N.launch_compress_linked(d, off, ln, link, out, oo, ln - 1, olen, nb, 1, mode=mode)
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            N.launch_compress_linked(d, off, ln, link, out, oo, ln - 1, olen, nb, 1, mode=mode)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t
+            res[name] = (dt, olen.clone())
+            print(f"{kind} {mib}MiB bsize={bsize} nb={nb} {name}: {dt*1e3:.1f} ms {n/dt/2**30:.3f} GiB/s"
+                  + (f" passes={L.lz4m_compress_linked_passes()}" if name == "spec" else ""), flush=True)
+        if "serial" in res:
+            print("  same lengths:", bool(torch.equal(res["spec"][1], res["serial"][1])), flush=True)
