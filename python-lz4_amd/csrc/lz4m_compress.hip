@@ -30,6 +30,21 @@ int pcompress_launch(const uint8_t* d_src, const int64_t* d_src_off, const int32
                      const int64_t* d_dst_off, const int32_t* d_dst_cap, int32_t* d_out_len, int64_t n, int variant,
                      hipStream_t stream);
 
+// Diagnostic build only (-DLZ4M_COMPRESS_PROF): wave-cycle sums per phase of
+// compress_block_w and event counts, read with lz4m_compress_prof.
+#ifdef LZ4M_COMPRESS_PROF
+__device__ unsigned long long g_cprof[32];
+#define CP_DECL uint64_t cp[16] = {0}; uint64_t cp_t = clock64();
+#define CP_MARK(i) do { const uint64_t _t = clock64(); cp[i] += _t - cp_t; cp_t = _t; } while (0)
+#define CP_COUNT(i, x) cp[i] += (uint64_t)(x)
+#define CP_FLUSH() do { if (lane == 0) for (int _i = 0; _i < 16; ++_i) atomicAdd(&g_cprof[_i], (unsigned long long)cp[_i]); } while (0)
+#else
+#define CP_DECL
+#define CP_MARK(i) do {} while (0)
+#define CP_COUNT(i, x) do {} while (0)
+#define CP_FLUSH() do {} while (0)
+#endif
+
 constexpr int kMinLength = 13;        // lz4.c:247
 constexpr int kLimit64K = 65536 + 11; // lz4.c:689
 constexpr int kMaxInput = 0x7E000000; // lz4.h:211
@@ -57,6 +72,7 @@ struct Table<LZ4M_TABLE_U16_HASH4> {   // 8192 x u16 (lz4.c:756-762, 839-843)
     __device__ static __forceinline__ uint32_t hash(const uint8_t* p) {
         return (ld32(p) * 2654435761u) >> (32 - 13);
     }
+    __device__ static __forceinline__ uint32_t hash_v(u32x4 v) { return (v.x * 2654435761u) >> (32 - 13); }
     __device__ static __forceinline__ uint32_t get(const uint16_t* t, uint32_t h) { return t[h]; }
     __device__ static __forceinline__ void put(uint16_t* t, uint32_t h, uint32_t v) { t[h] = (uint16_t)v; }
     // volatile: kept in program order, never forwarded (the probe reads back
@@ -75,6 +91,10 @@ struct Table<LZ4M_TABLE_U32_HASH5> {   // 4096 x u32 (lz4.c:764-774, 834-838)
     static constexpr int kEntries = 4096;
     __device__ static __forceinline__ uint32_t hash(const uint8_t* p) {
         return (uint32_t)(((ld64(p) << 24) * 889523592379ull) >> (64 - 12));
+    }
+    __device__ static __forceinline__ uint32_t hash_v(u32x4 v) {
+        const uint64_t x = ((uint64_t)v.y << 32) | v.x;
+        return (uint32_t)(((x << 24) * 889523592379ull) >> (64 - 12));
     }
     __device__ static __forceinline__ uint32_t get(const uint16_t* t, uint32_t h) {
         return reinterpret_cast<const uint32_t*>(t)[h];
@@ -122,6 +142,125 @@ __device__ __forceinline__ int64_t put_len(uint8_t* dst, int64_t op, int64_t len
     return op + n255 + 1;
 }
 
+// ---- source window ---------------------------------------------------------
+// The bytes around the parse position live in a 4 KiB LDS ring, refilled
+// 1 KiB at a time (16 B per lane) ahead of the parse, so the hash inputs, the
+// literal copies and the source side of catch-up / match counting are LDS
+// reads; only the candidate side (anywhere in the last 64 KiB) is read from
+// HBM / L2, 20 bytes per candidate, which settles the 4-byte check, a short
+// catch-up and a short match in one round trip.
+constexpr int kRing = 4096;
+constexpr int kChunk = 16 * kWave;
+constexpr int kRingBytes = kRing + 32;   // + a mirror of the first 32 bytes
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+
+struct Win {
+    lds_u8* r;
+    int32_t base;   // window position at ring offset 0 (the block start)
+    int32_t whi;    // resident: [max(base, whi - kRing), whi)
+    int32_t iend;
+    __device__ __forceinline__ bool has(int32_t p, int32_t len) const {
+#ifdef LZ4M_NO_RING
+        return false;
+#endif
+        return p >= base && p >= whi - kRing && p + len <= whi;
+    }
+};
+
+// bytes [p-4, p) -> pm and [p, p+16) -> v from the ring (p resident per has(p-4, 20))
+__device__ __forceinline__ void ring_fetch(const Win& W, int32_t p, uint32_t& pm, u32x4& v) {
+    const uint32_t i = (uint32_t)(p - W.base) & (kRing - 1);
+    const uint32_t sh = i & 3, j = i >> 2;
+    const lds_u32* R = (const lds_u32*)W.r;
+    const uint32_t a = R[(j - 1) & (kRing / 4 - 1)];
+    const uint32_t b = R[j], c = R[j + 1], d = R[j + 2], e = R[j + 3], f = R[j + 4];
+    pm = __builtin_amdgcn_alignbyte(b, a, sh);
+    v = u32x4{__builtin_amdgcn_alignbyte(c, b, sh), __builtin_amdgcn_alignbyte(d, c, sh),
+              __builtin_amdgcn_alignbyte(e, d, sh), __builtin_amdgcn_alignbyte(f, e, sh)};
+}
+
+__device__ __forceinline__ u32x4 ring_fetch16(const Win& W, int32_t p) {
+    const uint32_t i = (uint32_t)(p - W.base) & (kRing - 1);
+    const uint32_t sh = i & 3, j = i >> 2;
+    const lds_u32* R = (const lds_u32*)W.r;
+    const uint32_t b = R[j], c = R[j + 1], d = R[j + 2], e = R[j + 3], f = R[j + 4];
+    return u32x4{__builtin_amdgcn_alignbyte(c, b, sh), __builtin_amdgcn_alignbyte(d, c, sh),
+                 __builtin_amdgcn_alignbyte(e, d, sh), __builtin_amdgcn_alignbyte(f, e, sh)};
+}
+
+// a refill may overwrite ring bytes that are before `keep` (or before the block)
+__device__ __forceinline__ bool can_fill(const Win& W, int32_t keep) {
+    return W.whi < W.iend && W.whi - kRing + kChunk <= (keep > W.base ? keep : W.base);
+}
+// bytes [p, p+16) of the window for 0 <= p < iend; bytes at or past iend are
+// unspecified.  One unconditional load whose address is clamped into the
+// window (the caller's buffer may end at iend), realigned in registers --
+// loads in branches make the compiler wait for them at the join.
+__device__ __forceinline__ u32x4 shr_bytes(u32x4 r, uint32_t d) {
+    const uint32_t q = d >> 2, s = d & 3;
+    const uint32_t a0 = q == 0 ? r.x : q == 1 ? r.y : q == 2 ? r.z : r.w;
+    const uint32_t a1 = q == 0 ? r.y : q == 1 ? r.z : q == 2 ? r.w : 0u;
+    const uint32_t a2 = q == 0 ? r.z : q == 1 ? r.w : 0u;
+    const uint32_t a3 = q == 0 ? r.w : 0u;
+    return u32x4{__builtin_amdgcn_alignbyte(a1, a0, s), __builtin_amdgcn_alignbyte(a2, a1, s),
+                 __builtin_amdgcn_alignbyte(a3, a2, s), __builtin_amdgcn_alignbyte(0u, a3, s)};
+}
+__device__ __forceinline__ u32x4 ld16_win(const uint8_t* w, int32_t p, int32_t iend) {
+    if (iend < 16) return ld16_guarded(w + p, iend - p);   // tiny window (uniform)
+    const int32_t q = p < iend - 16 ? p : iend - 16;
+    return shr_bytes(ld16(w + q), (uint32_t)(p - q));
+}
+// the 4 bytes before window position p (bytes before the window start read
+// as 0); the window holds >= 4 bytes
+__device__ __forceinline__ uint32_t ld_before(const uint8_t* w, int32_t p) {
+    const uint32_t x = ld32(w + (p >= 4 ? p - 4 : 0));
+    return p >= 4 ? x : p <= 0 ? 0u : x << (8 * (4 - (uint32_t)p));
+}
+
+__device__ __forceinline__ u32x4 fill_load(const Win& W, const uint8_t* w, uint32_t lane) {
+    const int32_t p = W.whi + 16 * (int32_t)lane;
+    return ld16_win(w, p < W.iend ? p : W.iend - 1, W.iend);
+}
+__device__ __forceinline__ void fill_commit(Win& W, u32x4 v, uint32_t lane) {
+    const uint32_t o = (uint32_t)(W.whi - W.base + 16 * (int32_t)lane) & (kRing - 1);
+    lds_st16(W.r + o, v);
+    if (o < 32) lds_st16(W.r + kRing + o, v);
+    W.whi += kChunk;
+}
+// synchronous top-up until `need` is resident (or nothing more may be evicted)
+__device__ __forceinline__ void top_up(Win& W, const uint8_t* w, int32_t need, int32_t keep, uint32_t lane) {
+    while (W.whi < need && can_fill(W, keep)) fill_commit(W, fill_load(W, w, lane), lane);
+}
+
+// bytes [p-4, p) and [p, p+16) of the window: from the ring, or (some lane
+// outside it) from memory
+__device__ __forceinline__ void src_fetch(const Win& W, const uint8_t* w, int32_t p, uint32_t& pm, u32x4& v) {
+    const bool in = W.has(p - 4, 20);
+    ring_fetch(W, p, pm, v);
+    if (__any(!in)) {
+        const u32x4 gv = ld16_win(w, p, W.iend);
+        const uint32_t gm = ld_before(w, p);
+        if (!in) {
+            v = gv;
+            pm = gm;
+        }
+    }
+}
+
+// number of equal leading bytes of a ^ b over 12 bytes (the dwords y, z, w)
+__device__ __forceinline__ int eq12(u32x4 a, u32x4 b) {
+    const uint32_t x1 = a.y ^ b.y, x2 = a.z ^ b.z, x3 = a.w ^ b.w;
+    if (x1) return (int)(__builtin_ctz(x1) >> 3);
+    if (x2) return 4 + (int)(__builtin_ctz(x2) >> 3);
+    if (x3) return 8 + (int)(__builtin_ctz(x3) >> 3);
+    return 12;
+}
+
+__device__ __forceinline__ u32x4 readlane_x4(u32x4 v, int l) {
+    return u32x4{(uint32_t)__builtin_amdgcn_readlane((int)v.x, l), (uint32_t)__builtin_amdgcn_readlane((int)v.y, l),
+                 (uint32_t)__builtin_amdgcn_readlane((int)v.z, l), (uint32_t)__builtin_amdgcn_readlane((int)v.w, l)};
+}
+
 // Window form.  The block is w[hist .. hist+n); w[0 .. hist) is history the
 // parse may match into (a dictionary or the previous blocks of a linked
 // frame).  Table entries are indexes: window byte p has index ibase + p, so
@@ -135,9 +274,9 @@ __device__ __forceinline__ int64_t put_len(uint8_t* dst, int64_t op, int64_t len
 // dictionary; or carried over from the previous block).
 // oracle: orc_compress_window (oracle/lz4_oracle.c).
 template <int V>
-__device__ int64_t compress_block_w(const uint8_t* __restrict__ w, int64_t hist, int64_t n, uint8_t* dst,
-                                    int64_t cap, int accel, uint16_t* tab, uint32_t lane, uint32_t ibase,
-                                    uint32_t low_idx, int64_t low_src, int64_t low_dict) {
+__device__ int32_t compress_block_w(const uint8_t* __restrict__ w, int32_t hist, int32_t n, uint8_t* dst,
+                                    int32_t cap, int accel, uint16_t* tab, lds_u8* ring, uint32_t lane,
+                                    uint32_t ibase, uint32_t low_idx, int32_t low_src, int32_t low_dict) {
     using T = Table<V>;
     if (n > kMaxInput) return 0;                               // lz4.c:1324
     const bool limited = cap < bound64(n);
@@ -148,46 +287,68 @@ __device__ int64_t compress_block_w(const uint8_t* __restrict__ w, int64_t hist,
     }
     if (V == LZ4M_TABLE_U16_HASH4 && n >= kLimit64K) return 0;   // lz4.c:963
 
-    const int64_t iend = hist + n;
-    const int64_t mflimit1 = iend - 12 + 1;                     // lz4.c:942
-    const int64_t matchlimit = iend - 5;
+    const int32_t iend = hist + n;
+    const int32_t mflimit1 = iend - 12 + 1;                     // lz4.c:942
+    const int32_t matchlimit = iend - 5;
     const int64_t A = (int64_t)accel << 6;                      // searchMatchNb start
     const int64_t FA = skip_sum(A - 1);
-    int64_t anchor = hist, ip = hist, op = 0;
+    int32_t anchor = hist, ip = hist, op = 0;
+    Win W{ring, hist, hist, iend};
+    // the match being encoded: ip side P = [pbase, pbase+16), candidate side
+    // G = [gbase, gbase+16), back = bytes the catch-up moved before them
+    u32x4 P, G;
+    int32_t pbase = 0, gbase = 0, back = 0;
 
+    CP_DECL
     if (n < kMinLength) goto last_literals;                    // lz4.c:981
 
-    if (lane == 0) T::put(tab, T::hash(w + hist), ibase + (uint32_t)hist);   // lz4.c:984
-    __builtin_amdgcn_s_waitcnt(0xc07f);
+    top_up(W, w, hist + kRing, hist, lane);
+    if (lane == 0) T::put_v(tab, T::hash(w + hist), ibase + (uint32_t)hist);   // lz4.c:984
     ip = hist + 1;
 
     for (;;) {
-        int64_t match;
-        int64_t tok_pos;
+        int32_t match;
+        int32_t tok_pos;
+        uint32_t tok_hi;   // literal-length nibble; the token byte is written once, with the match nibble
+        uint32_t PM, GM;
         {   // ---- search (lz4.c:1016-1075), 64 attempts per wave step ----
             int64_t k0 = 0;
             for (;;) {
                 const int64_t k = k0 + lane;
-                const int64_t pos = ip + attempt_off(k, A, FA);
-                const int64_t nxt = ip + 1 + skip_sum(A + k - 1) - FA;   // position of attempt k+1
+                // attempts 0..63 of acceleration 1 are consecutive positions
+                const bool unit = A == 64 && k0 == 0;
+                const int64_t pos64 = ip + (unit ? k : attempt_off(k, A, FA));
+                const int64_t nxt = unit ? pos64 + 1 : ip + 1 + skip_sum(A + k - 1) - FA;   // attempt k+1
                 const bool valid = nxt <= mflimit1;
+                const int32_t pos = valid ? (int32_t)pos64 : ip;
                 const uint64_t vmask = __ballot(valid);
                 const int nvalid = __builtin_popcountll(vmask);   // valid lanes are a prefix
+                if (nvalid > 0) {
+                    const int32_t pmax = __builtin_amdgcn_readlane(pos, nvalid - 1);
+                    if (pmax + 16 > W.whi) top_up(W, w, pmax + 16 + kChunk, anchor - 8, lane);
+                }
+                uint32_t pm = 0;
+                u32x4 pv = u32x4{0, 0, 0, 0};
+                src_fetch(W, w, pos, pm, pv);
+                CP_COUNT(8, 1);
+                CP_COUNT(15, __builtin_popcountll(__ballot(valid && !W.has(pos - 4, 20))));
                 const uint32_t cur = ibase + (uint32_t)pos;
                 // read the bucket, then probe it with the lane id: a lane that
                 // does not read its own id back shares its hash with another
                 // lane of this step (one LDS round trip, in order per wave)
                 uint32_t h = 0, old = 0, rb = lane;
                 if (valid) {
-                    h = T::hash(w + pos);
+                    h = T::hash_v(pv);
                     old = T::get_v(tab, h);
                     T::put_v(tab, h, lane);
                     rb = T::get_v(tab, h);
                 }
+                CP_MARK(0);
                 // per hash group: nearest earlier (pred) and later (succ) lane
                 int pred = -1, succ = 1 << 20;
                 uint64_t todo = __ballot(rb != lane);
                 while (todo) {
+                    CP_COUNT(11, 1);
                     const int l = __builtin_ctzll(todo);
                     const uint32_t h0 = (uint32_t)__builtin_amdgcn_readlane((int)h, l);
                     const bool in = valid && h == h0;
@@ -200,59 +361,104 @@ __device__ int64_t compress_block_w(const uint8_t* __restrict__ w, int64_t hist,
                         succ = gt ? __builtin_ctzll(gt) : 1 << 20;
                     }
                 }
+                CP_MARK(1);
                 // the serial loop inserted an earlier lane of the group first
-                const uint32_t cand = pred >= 0 ? ibase + (uint32_t)(ip + attempt_off(k0 + pred, A, FA)) : old;
-                int64_t cpos = pos;
-                bool hit = false;
-                if (valid) {
-                    const bool bad = (T::kDistCheck && cand + 65535u < cur) || cand < low_idx;
-                    cpos = bad ? pos : (int64_t)cand - (int64_t)ibase;
-                    hit = !bad && ld32(w + cpos) == ld32(w + pos);
-                }
+                const uint32_t cand =
+                    pred >= 0 ? ibase + (uint32_t)(ip + (unit ? (int64_t)pred : attempt_off(k0 + pred, A, FA))) : old;
+                int32_t cpos = pos;
+                bool ok = false;
+                u32x4 gv = u32x4{0, 0, 0, 0};
+                uint32_t gm = 0;
+                ok = valid && !((T::kDistCheck && cand + 65535u < cur) || cand < low_idx);
+                if (ok) cpos = (int32_t)cand - (int32_t)ibase;
+                gv = ld16_win(w, cpos, iend);   // unconditional (cpos = pos when not ok)
+                gm = ld_before(w, cpos);
+                // refill the ring ahead of the parse under the same wait
+                const bool pf = W.whi < ip + (kRing - kChunk) && can_fill(W, anchor - 8);
+                u32x4 fv = u32x4{0, 0, 0, 0};
+                if (pf) fv = fill_load(W, w, lane);
+                const bool hit = ok && gv.x == pv.x;
                 const uint64_t hmask = __ballot(hit);
                 const int f = hmask ? __builtin_ctzll(hmask) : nvalid;   // last lane processed: f (or all valid)
                 // one write per touched bucket: the group's last lane <= f
                 // inserts its position; a group entirely after f restores
                 if (valid && (((int)lane <= f && succ > f) || ((int)lane > f && pred < 0)))
                     T::put_v(tab, h, (int)lane <= f ? cur : old);
+                if (pf) fill_commit(W, fv, lane);
+                CP_MARK(2);
                 if (hmask) {
-                    ip = readlane64(pos, f);
-                    match = readlane64(cpos, f);
+                    ip = __builtin_amdgcn_readlane(pos, f);
+                    match = __builtin_amdgcn_readlane(cpos, f);
+                    P = readlane_x4(pv, f);
+                    G = readlane_x4(gv, f);
+                    PM = (uint32_t)__builtin_amdgcn_readlane((int)pm, f);
+                    GM = (uint32_t)__builtin_amdgcn_readlane((int)gm, f);
                     break;
                 }
                 if (nvalid < kWave) goto last_literals;        // forwardIp > mflimitPlusOne
                 k0 += kWave;
             }
-            ip = uni64(ip);
-            match = uni64(match);
+            pbase = ip;
+            gbase = match;
         }
 
         {   // ---- backward catch-up (lz4.c:1080) ----
-            const int64_t low = match < hist ? low_dict : low_src;
-            for (;;) {
-                const int64_t a = ip - 1 - lane, b = match - 1 - lane;
-                const bool ok = a >= anchor && b >= low && w[a < 0 ? 0 : a] == w[b < 0 ? 0 : b];
-                const uint64_t m = __ballot(ok);
-                const int run = ~m == 0 ? kWave : (int)__builtin_ctzll(~m);   // leading lanes that extend
-                ip -= run;
-                match -= run;
-                if (run < kWave) break;
+            const int32_t low = match < hist ? low_dict : low_src;
+            const int32_t lim = (ip - anchor) < (match - low) ? (ip - anchor) : (match - low);
+            const uint32_t x = PM ^ GM;   // byte 3: ip[-1] vs match[-1]
+            int32_t r = x == 0 ? 4 : (int32_t)(__builtin_clz(x) >> 3);
+            if (r > lim) r = lim;
+            ip -= r;
+            match -= r;
+            if (r == 4 && lim > 4) {
+                CP_COUNT(13, 1);
+                for (;;) {
+                    const int32_t a = ip - 1 - lane, b = match - 1 - lane;
+                    const bool okc = a >= anchor && b >= low && w[a < 0 ? 0 : a] == w[b < 0 ? 0 : b];
+                    const uint64_t m = __ballot(okc);
+                    const int run = ~m == 0 ? kWave : (int)__builtin_ctzll(~m);   // leading lanes that extend
+                    ip -= run;
+                    match -= run;
+                    if (run < kWave) break;
+                }
             }
+            back = pbase - ip;
+            CP_MARK(3);
+            CP_COUNT(9, 1);
         }
 
         {   // ---- literal run (lz4.c:1083-1107) ----
-            const int64_t lit = ip - anchor;
+            const int32_t lit = ip - anchor;
             tok_pos = op;
             op += 1;
             if (limited && op + lit + (2 + 1 + 5) + lit / 255 > cap) return 0;
             if (lit >= 15) {
-                if (lane == 0) dst[tok_pos] = 15 << 4;
+                tok_hi = 15 << 4;
                 op = put_len(dst, op, lit - 15, lane);
-            } else if (lane == 0) {
-                dst[tok_pos] = (uint8_t)(lit << 4);
+            } else {
+                tok_hi = (uint32_t)lit << 4;
             }
-            wave_copy(dst + op, w + anchor, lit, cap - op, iend - anchor, lane);
+            uint8_t* d = dst + op;
+            const int32_t d_room = cap - op;
+            for (int32_t b0 = 0; b0 < lit; b0 += 16 * kWave) {
+                const int32_t q = b0 + 16 * (int32_t)lane;
+                if (q < lit) {
+                    const int32_t p = anchor + q;
+                    const bool in = W.has(p, 16);
+                    u32x4 v = ring_fetch16(W, p);
+                    if (__any(!in)) {
+                        const u32x4 gv = ld16_win(w, p, iend);
+                        if (!in) v = gv;
+                    }
+                    if (lit - q >= 16 || d_room - q >= 16) {
+                        st16(d + q, v);
+                    } else {
+                        for (int32_t j = 0; j < lit - q; ++j) d[q + j] = (uint8_t)byte_of(v, (int)j);
+                    }
+                }
+            }
             op += lit;
+            CP_MARK(4);
         }
 
     next_match:
@@ -263,44 +469,52 @@ __device__ int64_t compress_block_w(const uint8_t* __restrict__ w, int64_t hist,
                 dst[op + 1] = (uint8_t)(off >> 8);
             }
             op += 2;
-            // LZ4_count(ip+4, match+4, matchlimit), 4 bytes per lane; a match
-            // in the history runs on into the block (lz4.c:1141-1153)
-            int64_t mcode = 0;
-            const int64_t p = ip + 4, q = match + 4;
-            for (;;) {
-                const int64_t avail = matchlimit - (p + mcode);
-                const int64_t at = mcode + 4 * (int64_t)lane;
-                const int64_t rem = avail - 4 * (int64_t)lane;   // bytes this lane may compare
-                uint32_t x = 0xFFFFFFFFu;   // nonzero = mismatch within range
-                int lim = 0;
-                if (rem >= 4) {
-                    x = ld32(w + p + at) ^ ld32(w + q + at);
-                    lim = 4;
-                } else if (rem > 0) {
-                    uint32_t xa = 0, xb = 0;
-                    for (int j = 0; j < (int)rem; ++j) {
-                        xa |= (uint32_t)w[p + at + j] << (8 * j);
-                        xb |= (uint32_t)w[q + at + j] << (8 * j);
+            // LZ4_count(ip+4, match+4, matchlimit): bytes 4..15 of P/G first,
+            // then 4 bytes per lane from HBM; a match in the history runs on
+            // into the block (lz4.c:1141-1153) -- the window is contiguous
+            const int32_t avail = matchlimit - (pbase + 4);
+            int32_t c = eq12(P, G);
+            if (c > avail) c = avail;
+            int32_t mcode = back + c;
+            if (c == 12 && avail > 12) {
+                int32_t more = 0;
+                const int32_t p = pbase + 16, q = gbase + 16;
+                for (;;) {
+                    const int32_t av = matchlimit - (p + more);
+                    const int32_t at = more + 4 * (int32_t)lane;
+                    const int32_t rem = av - 4 * (int32_t)lane;   // bytes this lane may compare
+                    uint32_t x = 0xFFFFFFFFu;   // nonzero = mismatch within range
+                    int lim = 0;
+                    if (rem >= 4) {
+                        x = ld32(w + p + at) ^ ld32(w + q + at);
+                        lim = 4;
+                    } else if (rem > 0) {
+                        uint32_t xa = 0, xb = 0;
+                        for (int j = 0; j < (int)rem; ++j) {
+                            xa |= (uint32_t)w[p + at + j] << (8 * j);
+                            xb |= (uint32_t)w[q + at + j] << (8 * j);
+                        }
+                        x = xa ^ xb;
+                        lim = (int)rem;
                     }
-                    x = xa ^ xb;
-                    lim = (int)rem;
+                    int eq = lim;
+                    if (x != 0) {
+                        const int cz = (int)(__builtin_ctz(x) >> 3);
+                        eq = cz < lim ? cz : lim;
+                    }
+                    const uint64_t stop = __ballot(eq < 4);
+                    if (stop == 0) {
+                        more += 4 * kWave;
+                        continue;
+                    }
+                    const int fl = __builtin_ctzll(stop);
+                    more += 4 * (int32_t)fl + __builtin_amdgcn_readlane(eq, fl);
+                    break;
                 }
-                // lane's count of equal leading bytes (0..4), limited by range
-                int eq = lim;
-                if (x != 0) {
-                    const int cz = (int)(__builtin_ctz(x) >> 3);
-                    eq = cz < lim ? cz : lim;
-                }
-                const uint64_t stop = __ballot(eq < 4);
-                if (stop == 0) {
-                    mcode += 4 * kWave;
-                    continue;
-                }
-                const int fl = __builtin_ctzll(stop);
-                mcode += 4 * (int64_t)fl + __builtin_amdgcn_readlane(eq, fl);
-                break;
+                mcode += more;
+                CP_COUNT(12, 1);
             }
-            mcode = uni64(mcode);
+            mcode = (int32_t)uni((uint32_t)mcode);
             ip += mcode + 4;
             if (limited && op + (1 + 5) + (mcode + 240) / 255 > cap) return 0;
             uint32_t tok_lo;
@@ -310,38 +524,55 @@ __device__ int64_t compress_block_w(const uint8_t* __restrict__ w, int64_t hist,
             } else {
                 tok_lo = (uint32_t)mcode;
             }
-            if (lane == 0) dst[tok_pos] = (uint8_t)(dst[tok_pos] + tok_lo);
+            if (lane == 0) dst[tok_pos] = (uint8_t)(tok_hi + tok_lo);
+            CP_MARK(5);
         }
         anchor = ip;
         if (ip >= mflimit1) break;                             // lz4.c:1204
 
         {   // ---- fill table, test next position (lz4.c:1207-1258) ----
-            if (lane == 0) T::put(tab, T::hash(w + ip - 2), ibase + (uint32_t)(ip - 2));
-            __builtin_amdgcn_s_waitcnt(0xc07f);
-            const uint32_t h = T::hash(w + ip);
-            const uint32_t cand = uni(T::get(tab, h));
+            if (ip + 16 > W.whi) top_up(W, w, ip + 16 + kChunk, ip - 8, lane);
+            uint32_t pm;
+            u32x4 pv;
+            src_fetch(W, w, ip, pm, pv);
+            // bytes [ip-2, ip+6)
+            const u32x4 pv2 = u32x4{__builtin_amdgcn_alignbyte(pv.x, pm, 2), __builtin_amdgcn_alignbyte(pv.y, pv.x, 2),
+                                    0u, 0u};
+            const uint32_t h2 = T::hash_v(pv2);
+            const uint32_t h = T::hash_v(pv);
             const uint32_t cur = ibase + (uint32_t)ip;
-            __builtin_amdgcn_s_waitcnt(0xc07f);
-            if (lane == 0) T::put(tab, h, cur);
-            __builtin_amdgcn_s_waitcnt(0xc07f);
+            if (lane == 0) T::put_v(tab, h2, cur - 2u);
+            const uint32_t cand = uni(T::get_v(tab, h));
+            if (lane == 0) T::put_v(tab, h, cur);
             const bool ok = cand >= low_idx && (!T::kDistCheck || cand + 65535u >= cur);
-            const int64_t cpos = ok ? (int64_t)cand - (int64_t)ibase : ip;
-            if (ok && ld32(w + cpos) == ld32(w + ip)) {
-                match = cpos;
-                tok_pos = op;
-                if (lane == 0) dst[tok_pos] = 0;
-                op += 1;
-                goto next_match;
+            {
+                const int32_t cpos = ok ? (int32_t)cand - (int32_t)ibase : ip;
+                const u32x4 gv = ld16_win(w, cpos, iend);
+                if (ok && gv.x == pv.x) {
+                    match = cpos;
+                    P = pv;
+                    G = gv;
+                    pbase = ip;
+                    gbase = cpos;
+                    back = 0;
+                    tok_pos = op;
+                    tok_hi = 0;
+                    op += 1;
+                    CP_MARK(6);
+                    CP_COUNT(10, 1);
+                    goto next_match;
+                }
             }
+            CP_MARK(6);
         }
         ++ip;
     }
 
 last_literals:
     {   // lz4.c:1266-1293
-        const int64_t run = iend - anchor;
+        const int32_t run = iend - anchor;
         if (limited && op + run + 1 + (run + 255 - 15) / 255 > cap) return 0;
-        const int64_t tpos = op;
+        const int32_t tpos = op;
         op += 1;
         if (run >= 15) {
             if (lane == 0) dst[tpos] = 15 << 4;
@@ -352,6 +583,8 @@ last_literals:
         wave_copy(dst + op, w + anchor, run, cap - op, iend - anchor, lane);
         op += run;
     }
+    CP_MARK(7);
+    CP_FLUSH();
     return op;
 }
 
@@ -365,10 +598,11 @@ __device__ __forceinline__ void zero_table(uint16_t* tab, uint32_t lane) {
 // One block with a fresh table (LZ4_compress_generic_validated, noDict).
 template <int V>
 __device__ __forceinline__ int64_t compress_block(const uint8_t* __restrict__ src, int64_t n, uint8_t* dst,
-                                                  int64_t cap, int accel, uint16_t* tab, uint32_t lane) {
+                                                  int64_t cap, int accel, uint16_t* tab, lds_u8* ring,
+                                                  uint32_t lane) {
     if (n > kMaxInput) return 0;
     zero_table(tab, lane);
-    return compress_block_w<V>(src, 0, n, dst, cap, accel, tab, lane, 0u, 0u, 0, 0);
+    return compress_block_w<V>(src, 0, n, dst, cap, accel, tab, ring, lane, 0u, 0u, 0, 0);
 }
 
 template <int V>
@@ -379,10 +613,12 @@ __global__ __launch_bounds__(64) void compress_kernel(const uint8_t* __restrict_
                                                       const int32_t* __restrict__ dst_cap,
                                                       int32_t* __restrict__ out_len, int64_t n, int accel) {
     __shared__ __attribute__((aligned(16))) uint16_t tab[8192];
+    __shared__ __attribute__((aligned(16))) uint8_t ring_mem[kRingBytes];
+    lds_u8* ring = (lds_u8*)ring_mem;
     const uint32_t lane = threadIdx.x;
     for (int64_t b = blockIdx.x; b < n; b += gridDim.x) {
         const int64_t len = src_len[b];
-        const int64_t r = compress_block<V>(src + src_off[b], len, dst + dst_off[b], dst_cap[b], accel, tab, lane);
+        const int64_t r = compress_block<V>(src + src_off[b], len, dst + dst_off[b], dst_cap[b], accel, tab, ring, lane);
         if (lane == 0) out_len[b] = (int32_t)r;
     }
 }
@@ -395,16 +631,18 @@ __global__ __launch_bounds__(64) void compress_kernel_auto(const uint8_t* __rest
                                                            const int32_t* __restrict__ dst_cap,
                                                            int32_t* __restrict__ out_len, int64_t n, int accel) {
     __shared__ __attribute__((aligned(16))) uint16_t tab[8192];
+    __shared__ __attribute__((aligned(16))) uint8_t ring_mem[kRingBytes];
+    lds_u8* ring = (lds_u8*)ring_mem;
     const uint32_t lane = threadIdx.x;
     for (int64_t b = blockIdx.x; b < n; b += gridDim.x) {
         const int64_t len = src_len[b];
         int64_t r;
         if (len < kLimit64K)
             r = compress_block<LZ4M_TABLE_U16_HASH4>(src + src_off[b], len, dst + dst_off[b], dst_cap[b], accel,
-                                                     tab, lane);
+                                                     tab, ring, lane);
         else
             r = compress_block<LZ4M_TABLE_U32_HASH5>(src + src_off[b], len, dst + dst_off[b], dst_cap[b], accel,
-                                                     tab, lane);
+                                                     tab, ring, lane);
         if (lane == 0) out_len[b] = (int32_t)r;
     }
 }
@@ -429,6 +667,8 @@ __global__ __launch_bounds__(64) void compress_dict_kernel(const uint8_t* __rest
                                                            const int32_t* __restrict__ dst_cap,
                                                            int32_t* __restrict__ out_len, int64_t n, int accel) {
     __shared__ __attribute__((aligned(16))) uint16_t tab[8192];
+    __shared__ __attribute__((aligned(16))) uint8_t ring_mem[kRingBytes];
+    lds_u8* ring = (lds_u8*)ring_mem;
     uint32_t* t32 = reinterpret_cast<uint32_t*>(tab);
     const uint32_t lane = threadIdx.x;
     for (int64_t b = blockIdx.x; b < n; b += gridDim.x) {
@@ -438,10 +678,10 @@ __global__ __launch_bounds__(64) void compress_dict_kernel(const uint8_t* __rest
         int64_t r;
         zero_table(tab, lane);
         if (dl < 0) {
-            r = compress_block_w<LZ4M_TABLE_U32_HASH5>(s, 0, len, dst + dst_off[b], dst_cap[b], accel, tab, lane,
+            r = compress_block_w<LZ4M_TABLE_U32_HASH5>(s, 0, len, dst + dst_off[b], dst_cap[b], accel, tab, ring, lane,
                                                        0u, 0u, 0, 0);
         } else if (dl < 8) {   // no dictionary kept (lz4.c:1564-1566): prefix mode, dictSmall, offset 64 KiB
-            r = compress_block_w<LZ4M_TABLE_U32_HASH5>(s, 0, len, dst + dst_off[b], dst_cap[b], accel, tab, lane,
+            r = compress_block_w<LZ4M_TABLE_U32_HASH5>(s, 0, len, dst + dst_off[b], dst_cap[b], accel, tab, ring, lane,
                                                        kWin, kWin, 0, 0);
         } else {
             const int64_t dt = dl < (int64_t)kWin ? dl : (int64_t)kWin;
@@ -451,7 +691,7 @@ __global__ __launch_bounds__(64) void compress_dict_kernel(const uint8_t* __rest
             for (int64_t p = 3 * (int64_t)lane; p <= dt - 8; p += 3 * kWave)
                 atomicMax(&t32[TabU32::hash(w + p)], ibase + (uint32_t)p);
             __builtin_amdgcn_s_waitcnt(0xc07f);
-            r = compress_block_w<LZ4M_TABLE_U32_HASH5>(w, dt, len, dst + dst_off[b], dst_cap[b], accel, tab, lane,
+            r = compress_block_w<LZ4M_TABLE_U32_HASH5>(w, dt, len, dst + dst_off[b], dst_cap[b], accel, tab, ring, lane,
                                                        ibase, ibase, dt, 0);
         }
         if (lane == 0) out_len[b] = (int32_t)r;
@@ -472,6 +712,8 @@ __global__ __launch_bounds__(64) void compress_chain_kernel(const uint8_t* __res
                                                             const int32_t* __restrict__ dst_cap,
                                                             int32_t* __restrict__ out_len, int64_t n, int accel) {
     __shared__ __attribute__((aligned(16))) uint16_t tab[8192];
+    __shared__ __attribute__((aligned(16))) uint8_t ring_mem[kRingBytes];
+    lds_u8* ring = (lds_u8*)ring_mem;
     uint32_t* t32 = reinterpret_cast<uint32_t*>(tab);
     const uint32_t lane = threadIdx.x;
     for (int64_t b0 = blockIdx.x; b0 < n; b0 += gridDim.x) {
@@ -481,7 +723,9 @@ __global__ __launch_bounds__(64) void compress_chain_kernel(const uint8_t* __res
         uint32_t start = 0;
         for (int64_t b = b0; b < n && (b == b0 || link[b]); ++b) {
             const int64_t len = src_len[b];
-            if ((uint64_t)start + (uint64_t)len > 0x80000000ull) {
+            // renormalise well before the reference does (2 GB): the shift
+            // never changes a parse, and keeps window positions in int32
+            if ((uint64_t)start + (uint64_t)len > 0x40000000ull) {
                 const uint32_t delta = start - kWin;
                 for (int i = lane; i < 4096; i += kWave) {
                     const uint32_t v = t32[i];
@@ -491,9 +735,9 @@ __global__ __launch_bounds__(64) void compress_chain_kernel(const uint8_t* __res
                 w += delta;
                 start = kWin;
             }
-            const int64_t hist = (src + src_off[b]) - w;
-            const int64_t r = compress_block_w<LZ4M_TABLE_U32_HASH5>(w, hist, len, dst + dst_off[b], dst_cap[b],
-                                                                     accel, tab, lane, 0u, 0u, 0, 0);
+            const int32_t hist = (int32_t)((src + src_off[b]) - w);
+            const int32_t r = compress_block_w<LZ4M_TABLE_U32_HASH5>(w, hist, (int32_t)len, dst + dst_off[b], dst_cap[b],
+                                                                     accel, tab, ring, lane, 0u, 0u, 0, 0);
             if (lane == 0) out_len[b] = (int32_t)r;
             start += (uint32_t)len;
         }
@@ -522,6 +766,8 @@ __global__ __launch_bounds__(64) void compress_spec_kernel(
     const uint32_t* __restrict__ t_prev, uint32_t* __restrict__ t_cur, const uint8_t* __restrict__ chg_prev,
     uint8_t* __restrict__ chg_cur, int32_t* counters, int pass) {
     __shared__ __attribute__((aligned(16))) uint16_t tab[8192];
+    __shared__ __attribute__((aligned(16))) uint8_t ring_mem[kRingBytes];
+    lds_u8* ring = (lds_u8*)ring_mem;
     u32x4* t4 = reinterpret_cast<u32x4*>(tab);
     const uint32_t lane = threadIdx.x;
     for (int64_t b = blockIdx.x; b < n; b += gridDim.x) {
@@ -558,7 +804,7 @@ __global__ __launch_bounds__(64) void compress_spec_kernel(
         }
         const uint8_t* w = src + src_off[b] - hist;
         const int64_t r = compress_block_w<LZ4M_TABLE_U32_HASH5>(w, hist, len, dst + dst_off[b], dst_cap[b],
-                                                                 accel, tab, lane, 0u, 0u, 0, 0);
+                                                                 accel, tab, ring, lane, 0u, 0u, 0, 0);
         if (lane == 0) out_len[b] = (int32_t)r;
         if (!feeds) {
             if (lane == 0) chg_cur[b] = 0;
@@ -645,6 +891,21 @@ extern "C" int lz4m_compress_dict_batch(const uint8_t* d_src, const int64_t* d_s
     hipLaunchKernelGGL(compress_dict_kernel, dim3(grid), dim3(64), 0, (hipStream_t)stream, d_src, d_src_off,
                        d_src_len, d_dict_len, d_dst, d_dst_off, d_dst_cap, d_out_len, n, acceleration);
     return (int)hipGetLastError();
+}
+
+extern "C" int lz4m_compress_prof(unsigned long long* out, int reset) {
+#ifdef LZ4M_COMPRESS_PROF
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(lz4m::g_cprof), sizeof(unsigned long long) * 16);
+    if (e == hipSuccess && reset) {
+        unsigned long long z[32] = {0};
+        e = hipMemcpyToSymbol(HIP_SYMBOL(lz4m::g_cprof), z, sizeof(z));
+    }
+    return (int)e;
+#else
+    (void)out;
+    (void)reset;
+    return -1;
+#endif
 }
 
 static thread_local int g_linked_passes = 0;

@@ -32,7 +32,8 @@ orc = O.Oracle()
 blocks = [b.tobytes() for b in _synth.blocks(96, "silesia", seed=11)]
 variant = int(sys.argv[1]) if len(sys.argv) > 1 else 0
 dev = torch.device("cuda", 0)
-for bi in range(4):
+B0 = int(os.environ.get("B0", 0)); B1 = int(os.environ.get("B1", 4))
+for bi in range(B0, B1):
     g = gpu_compress([blocks[bi]], variant, dev)[0]
     w = orc.compress(blocks[bi], variant)
     sg, sw = seqs(g), seqs(w)
