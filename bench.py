@@ -564,7 +564,18 @@ def main():
             "decompress_frame_no_content_checksum_gib_s": round(world * L / fn_wall / GIB, 2),
             "note": "content XXH32 is one serial stream (SURVEY 0.5): a host core hashes the bytes streamed back "
                     "over PCIe while the device compresses / decodes (lz4m_xxh32_host_*)"}
-        del fsrc, frame, meta
+        # lz4.frame.compress's defaults (64 KiB linked blocks, the exact parse, byte-identical to the
+        # reference): speculative-parallel linked compression on a 256 MiB sample of the same input
+        LS = min(L, 256 << 20)
+        dl = {}
+        dl_wall, _ = time_kernel(lambda: dl.__setitem__("f", _compress_frame(fsrc, LS)), 1, 1, world)
+        dfr = dl.pop("f")[0]
+        assert torch.equal(F.decompress_device(dfr), fsrc[:LS]), "default linked frame does not round-trip"
+        extra["frame4m"]["compress_frame_default_linked_gib_s"] = round(world * LS / dl_wall / GIB, 3)
+        extra["frame4m"]["compress_frame_default_linked_sample_mib"] = LS >> 20
+        extra["frame4m"]["compress_frame_default_linked_passes"] = int(N.lib().lz4m_compress_linked_passes())
+        extra["frame4m"]["compress_frame_default_linked_ratio"] = round(LS / dfr.numel(), 4)
+        del dfr, fsrc, frame, meta
         torch.cuda.empty_cache()
 
     # ---- config 1: the per-call drop-in path (host bytes in, host bytes out) ----
