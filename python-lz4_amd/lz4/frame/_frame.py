@@ -513,6 +513,50 @@ def _decode_records(d_frame, info, nb, c_off, c_len, raw_mask, crc_pos):
 
 def _decode_linked(d_frame, c_off, c_len, raw_mask, out, status, maxb):
     """Linked blocks: each block may reference the previous output
-    (LZ4F_updateDict, lz4frame.c:1853-1856), so blocks decode in order on one
-    wavefront, contiguously into `out`."""
-    N.launch_decompress_chain(d_frame, c_off, c_len, raw_mask, out, status, c_off.numel(), maxb)
+    (LZ4F_updateDict, lz4frame.c:1853-1856: LZ4_decompress_safe_usingDict
+    with the last <= 64 KiB decoded), contiguously into `out`.
+
+    Speculatively in rounds: every block decodes at once with the previous
+    round's output as its dictionary (two buffers), until a round changes no
+    byte and no status.  At that fixed point block k was decoded with the
+    true output of block k-1 and, by induction from block 0 (no dictionary),
+    every block equals the serial chain's.  This needs every block but the
+    last to decode to exactly the block size (what LZ4F_compressFrame and the
+    lz4 tool write); otherwise, or with LZ4M_LINKED_DECODE=serial, blocks
+    decode in order on one wavefront (lz4m_decompress_chain)."""
+    nb = c_off.numel()
+    if nb <= 2 or os.environ.get("LZ4M_LINKED_DECODE", "") == "serial":
+        N.launch_decompress_chain(d_frame, c_off, c_len, raw_mask, out, status, nb, maxb)
+        return
+    dev = d_frame.device
+    span = nb * maxb
+    slot_off = torch.arange(nb, dtype=torch.int64, device=dev) * maxb
+    caps = torch.full((nb,), maxb, dtype=torch.int32, device=dev)
+    dec_len = torch.where(raw_mask, torch.zeros_like(c_len), c_len)
+    dlen = torch.clamp(slot_off, max=65536)
+    dict_off = slot_off - dlen
+    dlen = dlen.to(torch.int32)
+    bufs = [out, torch.zeros_like(out)]
+    sts = [torch.empty(nb, dtype=torch.int32, device=dev), torch.empty(nb, dtype=torch.int32, device=dev)]
+    sel_r = torch.nonzero(raw_mask).flatten()
+    for b in bufs:                                             # stored blocks: their bytes, every round
+        if sel_r.numel():
+            N.gather(d_frame, c_off[sel_r], c_len[sel_r], b, slot_off[sel_r], sel_r.numel())
+    cur = 0
+    for r in range(nb + 1):
+        prev = cur ^ 1
+        N.launch_decompress(d_frame, c_off, dec_len, bufs[cur], slot_off, caps, sts[cur], nb,
+                            dict_buf=bufs[prev], dict_off=dict_off, dict_len=dlen)
+        sts[cur] = torch.where(raw_mask, c_len, sts[cur])
+        if r > 0 and torch.equal(sts[cur], sts[prev]) and torch.equal(bufs[cur][:span], bufs[prev][:span]):
+            break
+        cur = prev
+    st = sts[cur]
+    bad = st < 0
+    upto = int(torch.nonzero(bad).flatten()[0]) if bool(bad.any()) else nb - 1
+    if upto > 0 and not bool((st[:upto] == maxb).all()):       # a short block mid-frame: positions differ
+        N.launch_decompress_chain(d_frame, c_off, c_len, raw_mask, out, status, nb, maxb)
+        return
+    if bufs[cur] is not out:
+        out[:span].copy_(bufs[cur][:span])
+    status.copy_(st)

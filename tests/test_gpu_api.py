@@ -325,6 +325,39 @@ def test_linked_mixed_streams(gpu, oracle):
         N.launch_compress_linked(d, off, ln, link, out, oo, cap, olen, nb, 1, mode=N.LINKED_SPECULATIVE)
 
 
+def _frame_bytes(blocks, linked=True, bsid=4):
+    """A frame from hand-made block records: (payload, raw) pairs."""
+    import oracle as O
+    flg = (1 << 6) | ((0 if linked else 1) << 5)
+    bd = bsid << 4
+    hdr = bytes([flg, bd])
+    hc = (O.Oracle().xxh32(hdr) >> 8) & 0xFF
+    out = struct.pack("<I", 0x184D2204) + hdr + bytes([hc])
+    for payload, raw in blocks:
+        out += struct.pack("<I", len(payload) | (0x80000000 if raw else 0)) + payload
+    return out + struct.pack("<I", 0)
+
+
+@pytest.mark.parametrize("mode", ["speculative", "serial"])
+def test_frame_linked_decode_modes(gpu, reference, monkeypatch, mode):
+    """Linked frames decode identically whichever way: speculative rounds
+    (every block but the last full) and the serial chain -- including a frame
+    whose stored short block mid-stream forces the serial path."""
+    from lz4 import _synth
+    if mode == "serial":
+        monkeypatch.setenv("LZ4M_LINKED_DECODE", "serial")
+    data = b"".join(_synth.blocks(3, k, seed=19).tobytes() for k in ("silesia", "text", "records", "runs"))
+    for bs in (4, 5):
+        f = lz4.frame.compress(data, block_size=bs, block_linked=True)
+        assert lz4.frame.decompress(f) == data
+    # block 0 independent, block 1 stored (100 B), block 2 compressed against the last 64 KiB
+    a, b, c = data[:65536], data[65536:65636], data[70000:135536]
+    b0 = reference.compress_dict(a, b"")   # any valid block decoding to a
+    b2 = reference.compress_dict(c, (a + b)[-65536:])
+    f = _frame_bytes([(b0, False), (b, True), (b2, False)])
+    assert lz4.frame.decompress(f) == a + b + c
+
+
 def test_frame_decodes_reference_frames(gpu, golden):
     man, arr = golden
     inputs = {e["name"]: _b(arr, e["key"]) for e in man["inputs"]}
