@@ -274,7 +274,7 @@ __device__ __forceinline__ u32x4 readlane_x4(u32x4 v, int l) {
 // dictionary; or carried over from the previous block).
 // oracle: orc_compress_window (oracle/lz4_oracle.c).
 template <int V>
-__device__ int32_t compress_block_w(const uint8_t* __restrict__ w, int32_t hist, int32_t n, uint8_t* dst,
+__device__ __forceinline__ int32_t compress_block_w(const uint8_t* __restrict__ w, int32_t hist, int32_t n, uint8_t* dst,
                                     int32_t cap, int accel, uint16_t* tab, lds_u8* ring, uint32_t lane,
                                     uint32_t ibase, uint32_t low_idx, int32_t low_src, int32_t low_dict) {
     using T = Table<V>;
@@ -605,44 +605,24 @@ __device__ __forceinline__ int64_t compress_block(const uint8_t* __restrict__ sr
     return compress_block_w<V>(src, 0, n, dst, cap, accel, tab, ring, lane, 0u, 0u, 0, 0);
 }
 
+// `only`: -1 every block; 0 only blocks < 65547 B; 1 only blocks >= 65547 B.
+// LZ4M_TABLE_AUTO launches the U16 kernel with 0 and the U32 kernel with 1
+// (lz4.c:1352-1357): one kernel holding both parses would need 196 VGPRs.
 template <int V>
 __global__ __launch_bounds__(64) void compress_kernel(const uint8_t* __restrict__ src,
                                                       const int64_t* __restrict__ src_off,
                                                       const int32_t* __restrict__ src_len, uint8_t* dst,
                                                       const int64_t* __restrict__ dst_off,
                                                       const int32_t* __restrict__ dst_cap,
-                                                      int32_t* __restrict__ out_len, int64_t n, int accel) {
+                                                      int32_t* __restrict__ out_len, int64_t n, int accel, int only) {
     __shared__ __attribute__((aligned(16))) uint16_t tab[8192];
     __shared__ __attribute__((aligned(16))) uint8_t ring_mem[kRingBytes];
     lds_u8* ring = (lds_u8*)ring_mem;
     const uint32_t lane = threadIdx.x;
     for (int64_t b = blockIdx.x; b < n; b += gridDim.x) {
         const int64_t len = src_len[b];
+        if (only >= 0 && (len >= kLimit64K) != (only == 1)) continue;
         const int64_t r = compress_block<V>(src + src_off[b], len, dst + dst_off[b], dst_cap[b], accel, tab, ring, lane);
-        if (lane == 0) out_len[b] = (int32_t)r;
-    }
-}
-
-// AUTO: U16 for blocks < 65547 B, U32 otherwise (lz4.c:1352-1357)
-__global__ __launch_bounds__(64) void compress_kernel_auto(const uint8_t* __restrict__ src,
-                                                           const int64_t* __restrict__ src_off,
-                                                           const int32_t* __restrict__ src_len, uint8_t* dst,
-                                                           const int64_t* __restrict__ dst_off,
-                                                           const int32_t* __restrict__ dst_cap,
-                                                           int32_t* __restrict__ out_len, int64_t n, int accel) {
-    __shared__ __attribute__((aligned(16))) uint16_t tab[8192];
-    __shared__ __attribute__((aligned(16))) uint8_t ring_mem[kRingBytes];
-    lds_u8* ring = (lds_u8*)ring_mem;
-    const uint32_t lane = threadIdx.x;
-    for (int64_t b = blockIdx.x; b < n; b += gridDim.x) {
-        const int64_t len = src_len[b];
-        int64_t r;
-        if (len < kLimit64K)
-            r = compress_block<LZ4M_TABLE_U16_HASH4>(src + src_off[b], len, dst + dst_off[b], dst_cap[b], accel,
-                                                     tab, ring, lane);
-        else
-            r = compress_block<LZ4M_TABLE_U32_HASH5>(src + src_off[b], len, dst + dst_off[b], dst_cap[b], accel,
-                                                     tab, ring, lane);
         if (lane == 0) out_len[b] = (int32_t)r;
     }
 }
@@ -675,25 +655,24 @@ __global__ __launch_bounds__(64) void compress_dict_kernel(const uint8_t* __rest
         const int64_t len = src_len[b];
         const int64_t dl = dict_len[b];
         const uint8_t* s = src + src_off[b];
-        int64_t r;
         zero_table(tab, lane);
-        if (dl < 0) {
-            r = compress_block_w<LZ4M_TABLE_U32_HASH5>(s, 0, len, dst + dst_off[b], dst_cap[b], accel, tab, ring, lane,
-                                                       0u, 0u, 0, 0);
-        } else if (dl < 8) {   // no dictionary kept (lz4.c:1564-1566): prefix mode, dictSmall, offset 64 KiB
-            r = compress_block_w<LZ4M_TABLE_U32_HASH5>(s, 0, len, dst + dst_off[b], dst_cap[b], accel, tab, ring, lane,
-                                                       kWin, kWin, 0, 0);
-        } else {
-            const int64_t dt = dl < (int64_t)kWin ? dl : (int64_t)kWin;
-            const uint8_t* w = s - dt;
-            const uint32_t ibase = kWin - (uint32_t)dt;
+        // one call site: the three modes differ only in window and index parameters
+        const uint8_t* w = s;
+        int32_t hist = 0;
+        uint32_t ibase = 0, low_idx = 0;
+        if (dl >= 0 && dl < 8) {   // no dictionary kept (lz4.c:1564-1566): prefix mode, dictSmall, offset 64 KiB
+            ibase = low_idx = kWin;
+        } else if (dl >= 8) {
+            hist = (int32_t)(dl < (int64_t)kWin ? dl : (int64_t)kWin);
+            w = s - hist;
+            ibase = low_idx = kWin - (uint32_t)hist;
             // every third position, later positions win (lz4.c:1575-1578)
-            for (int64_t p = 3 * (int64_t)lane; p <= dt - 8; p += 3 * kWave)
+            for (int32_t p = 3 * (int32_t)lane; p <= hist - 8; p += 3 * kWave)
                 atomicMax(&t32[TabU32::hash(w + p)], ibase + (uint32_t)p);
             __builtin_amdgcn_s_waitcnt(0xc07f);
-            r = compress_block_w<LZ4M_TABLE_U32_HASH5>(w, dt, len, dst + dst_off[b], dst_cap[b], accel, tab, ring, lane,
-                                                       ibase, ibase, dt, 0);
         }
+        const int32_t r = compress_block_w<LZ4M_TABLE_U32_HASH5>(w, hist, (int32_t)len, dst + dst_off[b], dst_cap[b],
+                                                                 accel, tab, ring, lane, ibase, low_idx, hist, 0);
         if (lane == 0) out_len[b] = (int32_t)r;
     }
 }
@@ -857,11 +836,11 @@ extern "C" int lz4m_compress_batch(const uint8_t* d_src, const int64_t* d_src_of
     switch (table) {
         case LZ4M_TABLE_U16_HASH4:
             hipLaunchKernelGGL(compress_kernel<LZ4M_TABLE_U16_HASH4>, dim3(grid), dim3(64), 0, s, d_src, d_src_off,
-                               d_src_len, d_dst, d_dst_off, d_dst_cap, d_out_len, n, acceleration);
+                               d_src_len, d_dst, d_dst_off, d_dst_cap, d_out_len, n, acceleration, -1);
             break;
         case LZ4M_TABLE_U32_HASH5:
             hipLaunchKernelGGL(compress_kernel<LZ4M_TABLE_U32_HASH5>, dim3(grid), dim3(64), 0, s, d_src, d_src_off,
-                               d_src_len, d_dst, d_dst_off, d_dst_cap, d_out_len, n, acceleration);
+                               d_src_len, d_dst, d_dst_off, d_dst_cap, d_out_len, n, acceleration, -1);
             break;
         case LZ4M_PARSE_PARALLEL:
             return pcompress_launch(d_src, d_src_off, d_src_len, d_dst, d_dst_off, d_dst_cap, d_out_len, n, 0, s);
@@ -870,8 +849,10 @@ extern "C" int lz4m_compress_batch(const uint8_t* d_src, const int64_t* d_src_of
         case LZ4M_PARSE_PARALLEL_LARGE:
             return pcompress_launch(d_src, d_src_off, d_src_len, d_dst, d_dst_off, d_dst_cap, d_out_len, n, 2, s);
         case LZ4M_TABLE_AUTO:
-            hipLaunchKernelGGL(compress_kernel_auto, dim3(grid), dim3(64), 0, s, d_src, d_src_off, d_src_len, d_dst,
-                               d_dst_off, d_dst_cap, d_out_len, n, acceleration);
+            hipLaunchKernelGGL(compress_kernel<LZ4M_TABLE_U16_HASH4>, dim3(grid), dim3(64), 0, s, d_src, d_src_off,
+                               d_src_len, d_dst, d_dst_off, d_dst_cap, d_out_len, n, acceleration, 0);
+            hipLaunchKernelGGL(compress_kernel<LZ4M_TABLE_U32_HASH5>, dim3(grid), dim3(64), 0, s, d_src, d_src_off,
+                               d_src_len, d_dst, d_dst_off, d_dst_cap, d_out_len, n, acceleration, 1);
             break;
         default:
             return LZ4M_EINVAL;

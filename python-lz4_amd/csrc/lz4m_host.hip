@@ -15,27 +15,46 @@
 namespace {
 
 constexpr int kMaxInput = 0x7E000000;   // LZ4_MAX_INPUT_SIZE, lz4.h:211
+constexpr size_t kMeta = 256;           // per-call record (offsets, sizes, result, decoder scratch)
 
+// Per-thread device buffer, pinned host staging buffer and stream, for the
+// device that is current when the call is made.  A call is then one
+// host-to-device copy of [input | record], the launch, one device-to-host
+// copy of [record | output] and one synchronisation.
 struct Scratch {
+    int dev = -1;
     uint8_t* buf = nullptr;
+    uint8_t* host = nullptr;
     size_t cap = 0;
     hipStream_t stream = nullptr;
-    ~Scratch() {
+    void release() {
         if (buf) (void)hipFree(buf);
+        if (host) (void)hipHostFree(host);
         if (stream) (void)hipStreamDestroy(stream);
+        buf = host = nullptr;
+        stream = nullptr;
+        cap = 0;
     }
-    // `bytes` of device memory (>= 256 B aligned pieces carved by the caller)
-    uint8_t* get(size_t bytes) {
-        if (stream == nullptr && hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    ~Scratch() { release(); }
+    bool get(size_t bytes) {
+        int d = 0;
+        if (hipGetDevice(&d) != hipSuccess) return false;
+        if (d != dev) {
+            release();
+            dev = d;
+        }
+        if (stream == nullptr && hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return false;
         if (bytes > cap) {
             if (buf) (void)hipFree(buf);
-            buf = nullptr;
+            if (host) (void)hipHostFree(host);
+            buf = host = nullptr;
             cap = 0;
             const size_t want = bytes + bytes / 4 + 4096;
-            if (hipMalloc(reinterpret_cast<void**>(&buf), want) != hipSuccess) return nullptr;
+            if (hipMalloc(reinterpret_cast<void**>(&buf), want) != hipSuccess) return false;
+            if (hipHostMalloc(reinterpret_cast<void**>(&host), want, hipHostMallocDefault) != hipSuccess) return false;
             cap = want;
         }
-        return buf;
+        return true;
     }
 };
 
@@ -43,31 +62,52 @@ thread_local Scratch t_scratch;
 
 inline size_t up(size_t x) { return (x + 255) & ~(size_t)255; }
 
-// one-block compress through lz4m_compress_batch; returns the compressed size or 0
+struct CMeta {
+    int64_t src_off, dst_off;
+    int32_t src_len, dst_cap, result, pad;
+    uint64_t work[8];   // decoder scratch (lz4m_decompress_workspace_bytes)
+};
+static_assert(sizeof(CMeta) <= kMeta, "record size");
+
+// One block through a batched entry point.  Layout (device and pinned host
+// alike): [input, up(len)] [record, kMeta] [output, cap]; copies in the first
+// two parts, runs `launch` on the record, copies back the last two.  Returns
+// the record's result (-1 if a HIP call failed; `fail` is returned then).
+template <typename Launch>
+int32_t one_block(const char* src, int32_t len, char* dst, int32_t cap, int32_t fail, Launch launch) {
+    const size_t in = up((size_t)len + 16);
+    if (!t_scratch.get(in + kMeta + (size_t)cap + 16)) return fail;
+    uint8_t* h = t_scratch.host;
+    uint8_t* d = t_scratch.buf;
+    if (len) memcpy(h, src, (size_t)len);
+    CMeta m{};
+    m.src_off = 0;
+    m.dst_off = (int64_t)(in + kMeta);
+    m.src_len = len;
+    m.dst_cap = cap;
+    m.result = fail;
+    memcpy(h + in, &m, sizeof m);
+    hipStream_t s = t_scratch.stream;
+    if (hipMemcpyAsync(d, h, in + kMeta, hipMemcpyHostToDevice, s) != hipSuccess) return fail;
+    CMeta* dm = reinterpret_cast<CMeta*>(d + in);
+    if (launch(d, dm, s) != 0) return fail;
+    // the output comes back in full (its size is known only on the device)
+    if (hipMemcpyAsync(h + in, d + in, kMeta + (size_t)cap, hipMemcpyDeviceToHost, s) != hipSuccess) return fail;
+    if (hipStreamSynchronize(s) != hipSuccess) return fail;
+    memcpy(&m, h + in, sizeof m);
+    if (m.result > 0 && m.result <= cap) memcpy(dst, h + in + kMeta, (size_t)m.result);
+    return m.result;
+}
+
+// one-block compress through the batched compressors; returns the compressed size or 0
 int compress_one(const char* src, char* dst, int srcSize, int dstCapacity, int table, int acceleration) {
     if (srcSize < 0 || srcSize > kMaxInput || dstCapacity < 0 || (srcSize > 0 && !src) || (dstCapacity > 0 && !dst))
         return 0;
-    const size_t need = up((size_t)srcSize + 16) + up((size_t)dstCapacity + 16) + 256;
-    uint8_t* d = t_scratch.get(need);
-    if (!d) return 0;
-    uint8_t* d_src = d;
-    uint8_t* d_dst = d + up((size_t)srcSize + 16);
-    uint8_t* d_meta = d_dst + up((size_t)dstCapacity + 16);
-    struct Meta {
-        int64_t src_off, dst_off;
-        int32_t src_len, dst_cap, out_len, pad;
-    } m{0, 0, srcSize, dstCapacity, 0, 0};
-    hipStream_t s = t_scratch.stream;
-    if (srcSize && hipMemcpyAsync(d_src, src, (size_t)srcSize, hipMemcpyHostToDevice, s) != hipSuccess) return 0;
-    if (hipMemcpyAsync(d_meta, &m, sizeof m, hipMemcpyHostToDevice, s) != hipSuccess) return 0;
-    Meta* dm = reinterpret_cast<Meta*>(d_meta);
-    if (lz4m_compress_batch(d_src, &dm->src_off, &dm->src_len, d_dst, &dm->dst_off, &dm->dst_cap, &dm->out_len, 1,
-                            table, acceleration, reinterpret_cast<lz4m_stream_t>(s)) != 0)
-        return 0;
-    if (hipMemcpyAsync(&m, d_meta, sizeof m, hipMemcpyDeviceToHost, s) != hipSuccess) return 0;
-    if (hipStreamSynchronize(s) != hipSuccess) return 0;
-    if (m.out_len > 0 && hipMemcpy(dst, d_dst, (size_t)m.out_len, hipMemcpyDeviceToHost) != hipSuccess) return 0;
-    return m.out_len;
+    const int32_t r = one_block(src, srcSize, dst, dstCapacity, 0, [&](uint8_t* d, CMeta* dm, hipStream_t s) {
+        return lz4m_compress_batch(d, &dm->src_off, &dm->src_len, d, &dm->dst_off, &dm->dst_cap, &dm->result, 1,
+                                   table, acceleration, reinterpret_cast<lz4m_stream_t>(s));
+    });
+    return r > 0 ? r : 0;
 }
 
 }  // namespace
@@ -75,29 +115,10 @@ int compress_one(const char* src, char* dst, int srcSize, int dstCapacity, int t
 extern "C" int lz4m_decompress_safe(const char* src, char* dst, int compressedSize, int dstCapacity) {
     if (compressedSize < 0 || dstCapacity < 0) return -1;
     if ((compressedSize > 0 && !src) || (dstCapacity > 0 && !dst)) return -1;
-    const size_t need = up((size_t)compressedSize + 16) + up((size_t)dstCapacity + 16) + 256;
-    uint8_t* d = t_scratch.get(need);
-    if (!d) return -1;
-    uint8_t* d_src = d;
-    uint8_t* d_dst = d + up((size_t)compressedSize + 16);
-    uint8_t* d_meta = d_dst + up((size_t)dstCapacity + 16);
-    struct Meta {
-        int64_t src_off, dst_off;
-        int32_t src_len, dst_cap, status, pad;
-        uint64_t work[8];
-    } m{0, 0, compressedSize, dstCapacity, -1, 0, {0, 0, 0, 0, 0, 0, 0, 0}};
-    hipStream_t s = t_scratch.stream;
-    if (compressedSize && hipMemcpyAsync(d_src, src, (size_t)compressedSize, hipMemcpyHostToDevice, s) != hipSuccess)
-        return -1;
-    if (hipMemcpyAsync(d_meta, &m, sizeof m, hipMemcpyHostToDevice, s) != hipSuccess) return -1;
-    Meta* dm = reinterpret_cast<Meta*>(d_meta);
-    if (lz4m_decompress_batch_ws(d_src, &dm->src_off, &dm->src_len, d_dst, &dm->dst_off, &dm->dst_cap, &dm->status, 1,
-                                 dm->work, sizeof m.work, reinterpret_cast<lz4m_stream_t>(s)) != 0)
-        return -1;
-    if (hipMemcpyAsync(&m, d_meta, sizeof m, hipMemcpyDeviceToHost, s) != hipSuccess) return -1;
-    if (hipStreamSynchronize(s) != hipSuccess) return -1;
-    if (m.status > 0 && hipMemcpy(dst, d_dst, (size_t)m.status, hipMemcpyDeviceToHost) != hipSuccess) return -1;
-    return m.status;
+    return one_block(src, compressedSize, dst, dstCapacity, -1, [&](uint8_t* d, CMeta* dm, hipStream_t s) {
+        return lz4m_decompress_batch_ws(d, &dm->src_off, &dm->src_len, d, &dm->dst_off, &dm->dst_cap, &dm->result, 1,
+                                        dm->work, sizeof dm->work, reinterpret_cast<lz4m_stream_t>(s));
+    });
 }
 
 extern "C" int lz4m_compress_default(const char* src, char* dst, int srcSize, int dstCapacity) {
@@ -110,8 +131,8 @@ extern "C" int lz4m_compress_block_api(const char* src, char* dst, int srcSize, 
 
 extern "C" uint32_t lz4m_xxh32(const void* input, size_t length, uint32_t seed) {
     if (length > 0 && !input) return 0;
-    uint8_t* d = t_scratch.get(up(length + 16) + 256);
-    if (!d) return 0;
+    if (!t_scratch.get(up(length + 16) + 256)) return 0;
+    uint8_t* d = t_scratch.buf;
     uint32_t* d_out = reinterpret_cast<uint32_t*>(d + up(length + 16));
     hipStream_t s = t_scratch.stream;
     if (length && hipMemcpyAsync(d, input, length, hipMemcpyHostToDevice, s) != hipSuccess) return 0;

@@ -10,6 +10,7 @@ path.
 """
 from __future__ import annotations
 
+import ctypes as C
 import operator
 
 import torch
@@ -72,6 +73,11 @@ def _mode_accel(mode, acceleration: int) -> int:
     raise ValueError(f"Invalid mode argument: {mode}. Must be one of: standard, fast, high_compression")
 
 
+def _addr(view: memoryview):
+    """Address of a contiguous host buffer (read-only ones too), None if empty."""
+    return int(np.frombuffer(view, dtype=np.uint8).ctypes.data) if view.nbytes else None
+
+
 def _i64(vals, dev) -> torch.Tensor:
     return torch.tensor(vals, dtype=torch.int64, device=dev)
 
@@ -103,6 +109,19 @@ def compress(source, mode="default", store_size=True, acceleration=1, compressio
         if d.nbytes > INT_MAX:
             raise OverflowError("Dictionary too large for LZ4 API")
     accel = _mode_accel(mode, acceleration)
+    if d is None:   # one call: lz4m_compress_block_api (one copy in, one launch, one copy out)
+        N.device()
+        n = src.nbytes
+        hdr = _HDR if store_size else 0
+        out = bytearray(hdr + max(N.compress_bound(n), 1))
+        optr = C.addressof((C.c_char * len(out)).from_buffer(out))
+        r = N.lib().lz4m_compress_block_api(_addr(src), optr + hdr, n, len(out) - hdr, accel)
+        if r <= 0:
+            raise LZ4BlockError("Compression failed")
+        if hdr:
+            out[:4] = n.to_bytes(4, "little")
+        del out[hdr + r:]
+        return out if return_bytearray else bytes(out)
     out = compress_many([src], accel=accel, store_size=bool(store_size), as_bytearray=bool(return_bytearray),
                         dict=d)[0]
     if out is None:
@@ -127,6 +146,29 @@ def decompress(source, uncompressed_size=-1, return_bytearray=False, dict=None):
         dview = _buffer(dict, "dict")
         if dview.nbytes > INT_MAX:
             raise OverflowError("Dictionary too large for LZ4 API")
+    if dview is None or not dview.nbytes:   # one call: lz4m_decompress_safe
+        N.device()
+        if uncompressed_size >= 0:
+            cap, skip = uncompressed_size, 0
+        else:
+            if src.nbytes < _HDR:
+                raise ValueError("Input source data size too small")
+            cap = int.from_bytes(src[:4], "little")
+            if cap > INT_MAX:
+                raise ValueError(f"Invalid size: 0x{cap}")
+            skip = _HDR
+        out = bytearray(max(cap, 1))
+        optr = C.addressof((C.c_char * len(out)).from_buffer(out))
+        sp = _addr(src)
+        r = N.lib().lz4m_decompress_safe(None if sp is None else sp + skip, optr, src.nbytes - skip, cap)
+        if r < 0:
+            raise LZ4BlockError(
+                "Decompression failed: corrupt input or insufficient space in destination buffer. "
+                f"Error code: {-r}")
+        if r != cap and uncompressed_size < 0:
+            raise LZ4BlockError(f"Decompressor wrote {r} bytes, but {cap} bytes expected from header")
+        del out[r:]
+        return out if return_bytearray else bytes(out)
     res = decompress_many([src], uncompressed_size=uncompressed_size, dict=dview,
                           as_bytearray=bool(return_bytearray), raise_errors=True)
     return res[0]
