@@ -143,15 +143,22 @@ __device__ __forceinline__ int64_t put_len(uint8_t* dst, int64_t op, int64_t len
 }
 
 // ---- source window ---------------------------------------------------------
-// The bytes around the parse position live in a 4 KiB LDS ring, refilled
+// The bytes around the parse position live in a 2 KiB LDS ring, refilled
 // 1 KiB at a time (16 B per lane) ahead of the parse, so the hash inputs, the
 // literal copies and the source side of catch-up / match counting are LDS
 // reads; only the candidate side (anywhere in the last 64 KiB) is read from
 // HBM / L2, 20 bytes per candidate, which settles the 4-byte check, a short
 // catch-up and a short match in one round trip.
-constexpr int kRing = 4096;
+#ifndef LZ4M_CRING
+#define LZ4M_CRING 2048
+#endif
+constexpr int kRing = LZ4M_CRING;
 constexpr int kChunk = 16 * kWave;
+#ifdef LZ4M_NO_RING
+constexpr int kRingBytes = 16;           // A/B builds: every source read from memory
+#else
 constexpr int kRingBytes = kRing + 32;   // + a mirror of the first 32 bytes
+#endif
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 
 struct Win {
@@ -169,6 +176,11 @@ struct Win {
 
 // bytes [p-4, p) -> pm and [p, p+16) -> v from the ring (p resident per has(p-4, 20))
 __device__ __forceinline__ void ring_fetch(const Win& W, int32_t p, uint32_t& pm, u32x4& v) {
+#ifdef LZ4M_NO_RING
+    pm = 0;
+    v = u32x4{0, 0, 0, 0};
+    return;
+#endif
     const uint32_t i = (uint32_t)(p - W.base) & (kRing - 1);
     const uint32_t sh = i & 3, j = i >> 2;
     const lds_u32* R = (const lds_u32*)W.r;
@@ -180,6 +192,9 @@ __device__ __forceinline__ void ring_fetch(const Win& W, int32_t p, uint32_t& pm
 }
 
 __device__ __forceinline__ u32x4 ring_fetch16(const Win& W, int32_t p) {
+#ifdef LZ4M_NO_RING
+    return u32x4{0, 0, 0, 0};
+#endif
     const uint32_t i = (uint32_t)(p - W.base) & (kRing - 1);
     const uint32_t sh = i & 3, j = i >> 2;
     const lds_u32* R = (const lds_u32*)W.r;
@@ -190,6 +205,9 @@ __device__ __forceinline__ u32x4 ring_fetch16(const Win& W, int32_t p) {
 
 // a refill may overwrite ring bytes that are before `keep` (or before the block)
 __device__ __forceinline__ bool can_fill(const Win& W, int32_t keep) {
+#ifdef LZ4M_NO_RING
+    return false;
+#endif
     return W.whi < W.iend && W.whi - kRing + kChunk <= (keep > W.base ? keep : W.base);
 }
 // bytes [p, p+16) of the window for 0 <= p < iend; bytes at or past iend are
