@@ -143,17 +143,23 @@ __device__ __forceinline__ int64_t put_len(uint8_t* dst, int64_t op, int64_t len
 }
 
 // ---- source window ---------------------------------------------------------
-// The bytes around the parse position live in a 2 KiB LDS ring, refilled
-// 1 KiB at a time (16 B per lane) ahead of the parse, so the hash inputs, the
+// The bytes around the parse position live in a 1 KiB LDS ring, refilled
+// 512 B at a time (8 B per lane) ahead of the parse, so the hash inputs, the
 // literal copies and the source side of catch-up / match counting are LDS
 // reads; only the candidate side (anywhere in the last 64 KiB) is read from
 // HBM / L2, 20 bytes per candidate, which settles the 4-byte check, a short
 // catch-up and a short match in one round trip.
 #ifndef LZ4M_CRING
-#define LZ4M_CRING 2048
+#define LZ4M_CRING 1024
 #endif
 constexpr int kRing = LZ4M_CRING;
-constexpr int kChunk = 16 * kWave;
+#ifndef LZ4M_CCHUNK
+#define LZ4M_CCHUNK 512
+#endif
+constexpr int kChunk = LZ4M_CCHUNK;      // refill unit: 16 or 8 bytes per lane
+constexpr int kLaneB = kChunk / kWave;
+static_assert(kLaneB == 16 || kLaneB == 8, "ring refill granularity");
+static_assert(kChunk <= kRing / 2, "ring too small for its refill unit");
 #ifdef LZ4M_NO_RING
 constexpr int kRingBytes = 16;           // A/B builds: every source read from memory
 #else
@@ -236,13 +242,19 @@ __device__ __forceinline__ uint32_t ld_before(const uint8_t* w, int32_t p) {
 }
 
 __device__ __forceinline__ u32x4 fill_load(const Win& W, const uint8_t* w, uint32_t lane) {
-    const int32_t p = W.whi + 16 * (int32_t)lane;
+    const int32_t p = W.whi + kLaneB * (int32_t)lane;
     return ld16_win(w, p < W.iend ? p : W.iend - 1, W.iend);
 }
 __device__ __forceinline__ void fill_commit(Win& W, u32x4 v, uint32_t lane) {
-    const uint32_t o = (uint32_t)(W.whi - W.base + 16 * (int32_t)lane) & (kRing - 1);
-    lds_st16(W.r + o, v);
-    if (o < 32) lds_st16(W.r + kRing + o, v);
+    const uint32_t o = (uint32_t)(W.whi - W.base + kLaneB * (int32_t)lane) & (kRing - 1);
+    if (kLaneB == 16) {
+        lds_st16(W.r + o, v);
+        if (o < 32) lds_st16(W.r + kRing + o, v);
+    } else {
+        const uint64_t x = ((uint64_t)v.y << 32) | v.x;
+        __builtin_memcpy((uint8_t*)(W.r + o), &x, 8);
+        if (o < 32) __builtin_memcpy((uint8_t*)(W.r + kRing + o), &x, 8);
+    }
     W.whi += kChunk;
 }
 // synchronous top-up until `need` is resident (or nothing more may be evicted)
