@@ -22,6 +22,9 @@
 // copies are coalesced 16-byte-per-lane copies; sequence headers are written
 // by lane 0.
 #include "lz4m_common.h"
+
+#include <stdio.h>
+#include <stdlib.h>
 #include "../../include/lz4m.h"
 
 namespace lz4m {
@@ -963,6 +966,7 @@ extern "C" int lz4m_compress_linked_batch(const uint8_t* d_src, const int64_t* d
         if (e == hipSuccess) e = hipStreamSynchronize(s);
         if (e != hipSuccess) return (int)e;
         if (h_counters[1]) return LZ4M_EINVAL;
+        if (getenv("LZ4M_SPEC_VERBOSE")) fprintf(stderr, "[lz4m] linked pass %d: %d tables changed\n", (int)pass, h_counters[0]);
         if (h_counters[0] == 0) return 0;
     }
     return 0;

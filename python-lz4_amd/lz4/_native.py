@@ -285,17 +285,23 @@ def xxh32_host(buf, seed: int = 0) -> int:
 _PIN = {}
 
 
-def xxh32_of_device(t: torch.Tensor, n: int, seed: int = 0, wait_stream=None, chunk: int = 64 << 20) -> int:
+def xxh32_of_device(t: torch.Tensor, n: int, seed: int = 0, wait_stream=None, chunk: int = 64 << 20,
+                    wait_event=None) -> int:
     """XXH32 of the first n bytes of a device tensor, hashed on a host core:
     chunks are copied to two pinned buffers on a side stream, each hashed
-    while the next one copies (PCIe ~50 GB/s against ~5-7 GB/s of hashing).
+    while the next one copies (PCIe ~50 GB/s against ~13 GB/s of hashing).
+    ``wait_event``: an event recorded when t was ready (preferred: a caller
+    running this in a thread records it before queueing more work), else
     ``wait_stream``: the stream that produced t (default: current)."""
     st = HostXXH32(seed)
     if n <= 0:
         return st.digest()
     dev = t.device
     side = torch.cuda.Stream(dev)
-    side.wait_stream(wait_stream if wait_stream is not None else torch.cuda.current_stream(dev))
+    if wait_event is not None:
+        side.wait_event(wait_event)
+    else:
+        side.wait_stream(wait_stream if wait_stream is not None else torch.cuda.current_stream(dev))
     key = (threading.get_ident(), chunk)
     bufs = _PIN.get(key)
     if bufs is None:

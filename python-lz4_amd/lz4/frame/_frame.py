@@ -263,7 +263,9 @@ def _compress_frame(d_src, n=None, *, compression_level=0, block_size=0, content
             hthread = _HashThread(lambda: N.xxh32_host(host_src))
             hthread.start()
         else:                        # device bytes: streamed back and hashed while the device compresses
-            hthread = _HashThread(lambda: N.xxh32_of_device(d_src, n, wait_stream=main))
+            ready = torch.cuda.Event()
+            ready.record(main)       # before the compression is queued: the copies must not wait for it
+            hthread = _HashThread(lambda: N.xxh32_of_device(d_src, n, wait_event=ready))
             hthread.start()
     if nb:
         raw_off = torch.arange(nb, dtype=torch.int64, device=dev) * bsize
