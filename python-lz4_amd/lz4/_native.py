@@ -283,6 +283,22 @@ def xxh32_host(buf, seed: int = 0) -> int:
 
 
 _PIN = {}
+_PIN_LOCK = threading.Lock()
+
+
+def _pinned_pair(chunk: int):
+    """Two pinned host buffers of `chunk` bytes from a process-wide pool
+    (pinning 128 MiB costs tens of ms: never per call or per thread)."""
+    with _PIN_LOCK:
+        free = _PIN.setdefault(chunk, [])
+        if free:
+            return free.pop()
+    return [torch.empty(chunk, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
+
+
+def _pinned_release(chunk: int, bufs) -> None:
+    with _PIN_LOCK:
+        _PIN.setdefault(chunk, []).append(bufs)
 
 
 def xxh32_of_device(t: torch.Tensor, n: int, seed: int = 0, wait_stream=None, chunk: int = 64 << 20,
@@ -302,10 +318,7 @@ def xxh32_of_device(t: torch.Tensor, n: int, seed: int = 0, wait_stream=None, ch
         side.wait_event(wait_event)
     else:
         side.wait_stream(wait_stream if wait_stream is not None else torch.cuda.current_stream(dev))
-    key = (threading.get_ident(), chunk)
-    bufs = _PIN.get(key)
-    if bufs is None:
-        bufs = _PIN[key] = [torch.empty(chunk, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
+    bufs = _pinned_pair(chunk)
     evs = [torch.cuda.Event(), torch.cuda.Event()]
     spans = [(lo, min(n, lo + chunk)) for lo in range(0, n, chunk)]
     flat = t.view(-1)
@@ -316,12 +329,17 @@ def xxh32_of_device(t: torch.Tensor, n: int, seed: int = 0, wait_stream=None, ch
             bufs[i & 1][: hi - lo].copy_(flat[lo:hi], non_blocking=True)
             evs[i & 1].record(side)
 
-    issue(0)
-    for i, (lo, hi) in enumerate(spans):
-        if i + 1 < len(spans):
-            issue(i + 1)   # its buffer was hashed in iteration i - 1
-        evs[i & 1].synchronize()
-        st.update_ptr(bufs[i & 1].data_ptr(), hi - lo)
+    try:
+        issue(0)
+        for i, (lo, hi) in enumerate(spans):
+            if i + 1 < len(spans):
+                issue(i + 1)   # its buffer was hashed in iteration i - 1
+            evs[i & 1].synchronize()
+            st.update_ptr(bufs[i & 1].data_ptr(), hi - lo)
+    finally:
+        for e in evs:
+            e.synchronize()
+        _pinned_release(chunk, bufs)
     return st.digest()
 
 
