@@ -221,3 +221,21 @@ def test_differential_vs_reference(oracle, reference):
         d = b[:rng.randrange(1, 70000)]
         if c:
             assert oracle.decompress(bytes(c), cap, dict_=d) == reference.decompress(bytes(c), cap, dict_=d)
+
+
+def test_host_sanitizers():
+    """the CPU restatement and the package's host XXH32
+    (lz4m_xxh32_host.c) under AddressSanitizer + UBSan (oracle/Makefile
+    `asan`, driver oracle/asan_check.c): exact-size buffers over valid,
+    truncated, mutated and garbage blocks, dict= and linked streams, XXH32
+    in random chunks."""
+    import shutil
+    import subprocess
+    if shutil.which("gcc") is None:
+        pytest.skip("no host C compiler")
+    root = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "oracle")
+    r = subprocess.run(["make", "-s", "-C", root, "asan"], capture_output=True, text=True, timeout=600)
+    if r.returncode != 0 and "cannot find" in (r.stderr or "") and "asan" in r.stderr:
+        pytest.skip("sanitizer runtime not installed")
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "asan_check: ok" in r.stdout
