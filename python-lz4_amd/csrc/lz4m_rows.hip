@@ -196,7 +196,15 @@ __device__ __forceinline__ uint32_t dword_at(u32x4 w, uint32_t k) {
 // leave for HBM 32 at a time.
 constexpr int kPW = 128;                // ring bytes
 constexpr int kPWS = kPW + 16;          // ring + mirror
-constexpr int kPStage = 64;             // length ring (flushed in halves)
+#ifndef LZ4M_PARSE_STAGE
+#define LZ4M_PARSE_STAGE 32
+#endif
+constexpr int kPStage = LZ4M_PARSE_STAGE;   // length ring (flushed in halves)
+static_assert(kPStage == 32 || kPStage == 64, "length ring: 32 or 64 entries");
+#ifndef LZ4M_PARSE_WG
+#define LZ4M_PARSE_WG 64
+#endif
+constexpr int kPWG = LZ4M_PARSE_WG;     // parse workgroup (LDS is allocated per workgroup)
 #ifndef LZ4M_PARSE_MIN_ACTIVE
 #define LZ4M_PARSE_MIN_ACTIVE 40        // run the general step once fewer lanes than this can go on
 #endif
@@ -216,14 +224,14 @@ __device__ __forceinline__ void load64(const uint8_t* s, int32_t x, int32_t iend
     }
 }
 
-__global__ __launch_bounds__(256) void rows_parse_kernel(const uint8_t* __restrict__ src,
+__global__ __launch_bounds__(kPWG) void rows_parse_kernel(const uint8_t* __restrict__ src,
                                                          const int64_t* __restrict__ src_off,
                                                          const int32_t* __restrict__ src_len,
                                                          const int32_t* __restrict__ dst_cap, int64_t n,
                                                          RowMeta* __restrict__ meta, uint8_t* __restrict__ lens,
                                                          int64_t lens_cap, unsigned long long* __restrict__ ctr) {
-    __shared__ __attribute__((aligned(16))) uint8_t wins[256 * kPWS];
-    __shared__ __attribute__((aligned(16))) uint8_t stgs[256 * kPStage];
+    __shared__ __attribute__((aligned(16))) uint8_t wins[kPWG * kPWS];
+    __shared__ __attribute__((aligned(16))) uint8_t stgs[kPWG * kPStage];
     const uint32_t lane = lane_id();
     lds_u8* W = (lds_u8*)(wins + threadIdx.x * kPWS);
     lds_u8* stg = (lds_u8*)(stgs + threadIdx.x * kPStage);
@@ -370,17 +378,17 @@ __global__ __launch_bounds__(256) void rows_parse_kernel(const uint8_t* __restri
                 op += (int32_t)(lit + ml);
                 ++k;
             } else {   // the first sequence that is not good: the finisher resumes here
-                for (int32_t c = kf; c < k; c += 16) gbl_put(lens + loff + c, lds_ld16(stg + (c & 63)), k - c);
+                for (int32_t c = kf; c < k; c += 16) gbl_put(lens + loff + c, lds_ld16(stg + (c & (kPStage - 1))), k - c);
                 meta[idx] = RowMeta{loff, k, ip, op, 0, 0};
                 live = false;
             }
         }
         // flush full halves of the length ring
-        if (live && k - kf >= 32) {
+        if (live && k - kf >= kPStage / 2) {
             uint8_t* o = lens + loff + kf;
-            st16(o, lds_ld16(stg + (kf & 63)));
-            st16(o + 16, lds_ld16(stg + (kf & 63) + 16));
-            kf += 32;
+            st16(o, lds_ld16(stg + (kf & (kPStage - 1))));
+            if (kPStage == 64) st16(o + 16, lds_ld16(stg + (kf & (kPStage - 1)) + 16));
+            kf += kPStage / 2;
         }
         // request the next 64 bytes ahead
         if (live && !pfv && wb + kPW < iend) {
@@ -641,7 +649,12 @@ __global__ __launch_bounds__(64) void rows_exec_kernel(const uint8_t* __restrict
             b = ((unsigned long long)bhi << 32) | blo;
             if (b >= (unsigned long long)n) break;
             const RowMeta mt = meta[b];
-            if (mt.nseq == 0) continue;   // the finisher decodes the whole block
+            RP_COUNT(23, 1);
+            if (mt.nseq == 0) {   // the finisher decodes the whole block
+                RP_COUNT(24, 1);
+                RP_MARK(22);
+                continue;
+            }
             s = src + src_off[b];
             d = dst + dst_off[b];
             iend = src_len[b];
@@ -670,6 +683,7 @@ __global__ __launch_bounds__(64) void rows_exec_kernel(const uint8_t* __restrict
             if (k0 >= nseq) {   // the block's good prefix is done: flush the rest exactly
                 for (int32_t c = F + 16 * jj; c < op; c += 256) gbl_put(d + c, lds_ld16(HB + (c - base)), op - c);
                 have = false;
+                RP_MARK(20);
                 continue;
             }
             // one sequence that does not fit the buffers: flush, copy it in
@@ -709,6 +723,8 @@ __global__ __launch_bounds__(64) void rows_exec_kernel(const uint8_t* __restrict
             // op < oend - 64: the 16-byte reads stay inside the block's slot
             for (int32_t c = base + 16 * jj; c < op; c += 256) lds_st16(HB + (c - base), ld16(d + c));
             F = op;
+            RP_COUNT(25, 1);
+            RP_MARK(21);
             continue;
         }
         RP_MARK(10);
@@ -811,7 +827,7 @@ __global__ __launch_bounds__(64) void rows_exec_kernel(const uint8_t* __restrict
         }
         RP_MARK(9);
     }
-    RP_FLUSH(8, 24);
+    RP_FLUSH(8, 32);
 }
 
 }  // namespace lz4m
@@ -842,7 +858,7 @@ extern "C" int lz4m_rows_launch(const uint8_t* d_src, const int64_t* d_src_off, 
     const int64_t lens_cap = (int64_t)(work_bytes - fixed);
     hipError_t e = hipMemsetAsync(ctr, 0, 64, stream);
     if (e != hipSuccess) return (int)e;
-    hipLaunchKernelGGL(rows_parse_kernel, dim3((uint32_t)parse_grid), dim3(256), 0, stream, d_src, d_src_off,
+    hipLaunchKernelGGL(rows_parse_kernel, dim3((uint32_t)parse_grid), dim3(kPWG), 0, stream, d_src, d_src_off,
                        d_src_len, d_dst_cap, n, meta, lens, lens_cap, ctr);
     hipLaunchKernelGGL(rows_exec_kernel, dim3((uint32_t)exec_grid), dim3(64), 0, stream, d_src, d_src_off, d_src_len,
                        d_dst, d_dst_off, meta, lens, n, ctr);
@@ -853,11 +869,11 @@ extern "C" int lz4m_rows_grids(int64_t n, int* parse_grid, int* exec_grid) {
     int dev = 0, cus = 0, pk = 0, ek = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&pk, reinterpret_cast<const void*>(rows_parse_kernel), 256, 0);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&pk, reinterpret_cast<const void*>(rows_parse_kernel), kPWG, 0);
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&ek, reinterpret_cast<const void*>(rows_exec_kernel), 64, 0);
     if (cus <= 0) cus = 256;
     const int64_t ps = (int64_t)cus * (pk > 0 ? pk : 1), es = (int64_t)cus * (ek > 0 ? ek : 1);
-    const int64_t pneed = (n + 255) / 256, eneed = (n + 3) / 4;
+    const int64_t pneed = (n + kPWG - 1) / kPWG, eneed = (n + 3) / 4;
     *parse_grid = (int)(pneed < ps ? pneed : ps);
     *exec_grid = (int)(eneed < es ? eneed : es);
     return 0;

@@ -17,7 +17,7 @@ dev = torch.device("cuda", 0)
 lib = N.lib()
 PN = {0: "assign", 1: "general step", 2: "fast loop"}
 EN = {14: "block grab", 8: "sync parse", 10: "use==0 paths", 11: "parse ahead", 12: "literal",
-      13: "passes", 9: "flush+rebase"}
+      13: "passes", 9: "flush+rebase", 20: "block end flush", 21: "non-fit copy", 22: "nseq0 skip"}
 for kind in os.environ.get("KINDS", "silesia").split(","):
     nb = int(os.environ.get("NB", "262144"))
     src = B.make_batch(nb, min(4096, nb), kind, 7, dev)
@@ -46,6 +46,7 @@ for kind in os.environ.get("KINDS", "silesia").split(","):
     rounds = max(v[16], 1)
     print(f"  exec: rounds {v[16]} seqs/round(row0) {v[18] / rounds:.1f} passes/round {v[17] / rounds:.2f} "
           f"sync-load rounds {v[19] / 16 / rounds:.3f} cycles/round {et / rounds:.0f}")
+    print(f"  blocks grabbed {v[23]} nseq0 {v[24]} non-fit seqs {v[25]}")
     for i in EN:
         print(f"     {EN[i]:>14}: {100 * v[i] / max(et, 1):5.1f} %  {v[i] / rounds:7.0f} cyc/round")
     del src, slots, dst
