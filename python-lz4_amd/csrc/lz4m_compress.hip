@@ -66,6 +66,9 @@ __device__ __forceinline__ int64_t attempt_off(int64_t k, int64_t A, int64_t FA)
     return k >= 1 ? 1 + skip_sum(A + k - 2) - FA : 0;
 }
 
+typedef __attribute__((address_space(3))) uint16_t lds_t16;   // hash-table entries in LDS
+typedef __attribute__((address_space(3))) uint32_t lds_t32;
+
 template <int V>
 struct Table;
 
@@ -76,15 +79,15 @@ struct Table<LZ4M_TABLE_U16_HASH4> {   // 8192 x u16 (lz4.c:756-762, 839-843)
         return (ld32(p) * 2654435761u) >> (32 - 13);
     }
     __device__ static __forceinline__ uint32_t hash_v(u32x4 v) { return (v.x * 2654435761u) >> (32 - 13); }
-    __device__ static __forceinline__ uint32_t get(const uint16_t* t, uint32_t h) { return t[h]; }
-    __device__ static __forceinline__ void put(uint16_t* t, uint32_t h, uint32_t v) { t[h] = (uint16_t)v; }
+    __device__ static __forceinline__ uint32_t get(const uint16_t* t, uint32_t h) { return ((const lds_t16*)t)[h]; }
+    __device__ static __forceinline__ void put(uint16_t* t, uint32_t h, uint32_t v) { ((lds_t16*)t)[h] = (uint16_t)v; }
     // volatile: kept in program order, never forwarded (the probe reads back
-    // what OTHER lanes wrote)
-    __device__ static __forceinline__ uint32_t get_v(uint16_t* t, uint32_t h) {
-        return reinterpret_cast<volatile uint16_t*>(t)[h];
-    }
+    // what OTHER lanes wrote).  The table is in LDS: the accesses are cast to
+    // the LDS address space, else a volatile access through the generic
+    // pointer is a FLAT instruction that waits for every outstanding load.
+    __device__ static __forceinline__ uint32_t get_v(uint16_t* t, uint32_t h) { return ((volatile lds_t16*)t)[h]; }
     __device__ static __forceinline__ void put_v(uint16_t* t, uint32_t h, uint32_t v) {
-        reinterpret_cast<volatile uint16_t*>(t)[h] = (uint16_t)v;
+        ((volatile lds_t16*)t)[h] = (uint16_t)v;
     }
     static constexpr bool kDistCheck = false;   // lz4.c:1064, LZ4_DISTANCE_MAX == 65535
 };
@@ -99,18 +102,10 @@ struct Table<LZ4M_TABLE_U32_HASH5> {   // 4096 x u32 (lz4.c:764-774, 834-838)
         const uint64_t x = ((uint64_t)v.y << 32) | v.x;
         return (uint32_t)(((x << 24) * 889523592379ull) >> (64 - 12));
     }
-    __device__ static __forceinline__ uint32_t get(const uint16_t* t, uint32_t h) {
-        return reinterpret_cast<const uint32_t*>(t)[h];
-    }
-    __device__ static __forceinline__ void put(uint16_t* t, uint32_t h, uint32_t v) {
-        reinterpret_cast<uint32_t*>(t)[h] = v;
-    }
-    __device__ static __forceinline__ uint32_t get_v(uint16_t* t, uint32_t h) {
-        return reinterpret_cast<volatile uint32_t*>(t)[h];
-    }
-    __device__ static __forceinline__ void put_v(uint16_t* t, uint32_t h, uint32_t v) {
-        reinterpret_cast<volatile uint32_t*>(t)[h] = v;
-    }
+    __device__ static __forceinline__ uint32_t get(const uint16_t* t, uint32_t h) { return ((const lds_t32*)t)[h]; }
+    __device__ static __forceinline__ void put(uint16_t* t, uint32_t h, uint32_t v) { ((lds_t32*)t)[h] = v; }
+    __device__ static __forceinline__ uint32_t get_v(uint16_t* t, uint32_t h) { return ((volatile lds_t32*)t)[h]; }
+    __device__ static __forceinline__ void put_v(uint16_t* t, uint32_t h, uint32_t v) { ((volatile lds_t32*)t)[h] = v; }
     static constexpr bool kDistCheck = true;
 };
 
@@ -169,6 +164,13 @@ constexpr int kRingBytes = 16;           // A/B builds: every source read from m
 constexpr int kRingBytes = kRing + 32;   // + a mirror of the first 32 bytes
 #endif
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
+#ifdef LZ4M_NO_RING   // A/B: no ring in LDS at all (the 16 KiB table alone, 10 waves per CU)
+#define RING_DECL lds_u8* ring = nullptr;
+#else
+#define RING_DECL                                                               \
+    __shared__ __attribute__((aligned(16))) uint8_t ring_mem[kRingBytes];       \
+    lds_u8* ring = (lds_u8*)ring_mem;
+#endif
 
 struct Win {
     lds_u8* r;
@@ -404,12 +406,12 @@ __device__ __forceinline__ int32_t compress_block_w(const uint8_t* __restrict__ 
                 uint32_t gm = 0;
                 ok = valid && !((T::kDistCheck && cand + 65535u < cur) || cand < low_idx);
                 if (ok) cpos = (int32_t)cand - (int32_t)ibase;
-                gv = ld16_win(w, cpos, iend);   // unconditional (cpos = pos when not ok)
-                gm = ld_before(w, cpos);
                 // refill the ring ahead of the parse under the same wait
                 const bool pf = W.whi < ip + (kRing - kChunk) && can_fill(W, anchor - 8);
                 u32x4 fv = u32x4{0, 0, 0, 0};
                 if (pf) fv = fill_load(W, w, lane);
+                gv = ld16_win(w, cpos, iend);   // unconditional (cpos = pos when not ok)
+                gm = ld_before(w, cpos);
                 const bool hit = ok && gv.x == pv.x;
                 const uint64_t hmask = __ballot(hit);
                 const int f = hmask ? __builtin_ctzll(hmask) : nvalid;   // last lane processed: f (or all valid)
@@ -649,8 +651,7 @@ __global__ __launch_bounds__(64) void compress_kernel(const uint8_t* __restrict_
                                                       const int32_t* __restrict__ dst_cap,
                                                       int32_t* __restrict__ out_len, int64_t n, int accel, int only) {
     __shared__ __attribute__((aligned(16))) uint16_t tab[8192];
-    __shared__ __attribute__((aligned(16))) uint8_t ring_mem[kRingBytes];
-    lds_u8* ring = (lds_u8*)ring_mem;
+    RING_DECL
     const uint32_t lane = threadIdx.x;
     for (int64_t b = blockIdx.x; b < n; b += gridDim.x) {
         const int64_t len = src_len[b];
@@ -680,8 +681,7 @@ __global__ __launch_bounds__(64) void compress_dict_kernel(const uint8_t* __rest
                                                            const int32_t* __restrict__ dst_cap,
                                                            int32_t* __restrict__ out_len, int64_t n, int accel) {
     __shared__ __attribute__((aligned(16))) uint16_t tab[8192];
-    __shared__ __attribute__((aligned(16))) uint8_t ring_mem[kRingBytes];
-    lds_u8* ring = (lds_u8*)ring_mem;
+    RING_DECL
     uint32_t* t32 = reinterpret_cast<uint32_t*>(tab);
     const uint32_t lane = threadIdx.x;
     for (int64_t b = blockIdx.x; b < n; b += gridDim.x) {
@@ -724,8 +724,7 @@ __global__ __launch_bounds__(64) void compress_chain_kernel(const uint8_t* __res
                                                             const int32_t* __restrict__ dst_cap,
                                                             int32_t* __restrict__ out_len, int64_t n, int accel) {
     __shared__ __attribute__((aligned(16))) uint16_t tab[8192];
-    __shared__ __attribute__((aligned(16))) uint8_t ring_mem[kRingBytes];
-    lds_u8* ring = (lds_u8*)ring_mem;
+    RING_DECL
     uint32_t* t32 = reinterpret_cast<uint32_t*>(tab);
     const uint32_t lane = threadIdx.x;
     for (int64_t b0 = blockIdx.x; b0 < n; b0 += gridDim.x) {
@@ -778,8 +777,7 @@ __global__ __launch_bounds__(64) void compress_spec_kernel(
     const uint32_t* __restrict__ t_prev, uint32_t* __restrict__ t_cur, const uint8_t* __restrict__ chg_prev,
     uint8_t* __restrict__ chg_cur, int32_t* counters, int pass) {
     __shared__ __attribute__((aligned(16))) uint16_t tab[8192];
-    __shared__ __attribute__((aligned(16))) uint8_t ring_mem[kRingBytes];
-    lds_u8* ring = (lds_u8*)ring_mem;
+    RING_DECL
     u32x4* t4 = reinterpret_cast<u32x4*>(tab);
     const uint32_t lane = threadIdx.x;
     for (int64_t b = blockIdx.x; b < n; b += gridDim.x) {

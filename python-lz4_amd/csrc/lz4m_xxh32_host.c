@@ -9,6 +9,8 @@
  * (xxhash.c:263-286 primes/round/avalanche, :290-348 tail, :437-554 the
  * streaming state; state layout xxhash.h:264-274, total length mod 2^32).
  *
+ * Built with -fno-tree-vectorize: gcc turns the four accumulators into
+ * SSE2 lanes with an emulated 32-bit multiply (1.9 GB/s instead of ~14).
  * Kept in its own C file so that it builds without the HIP toolchain: the
  * host sanitizer build (oracle/Makefile `asan`) compiles it with
  * -fsanitize=address,undefined next to the CPU restatement.
