@@ -179,6 +179,23 @@ int lz4m_decompress_batch_dict(const uint8_t* d_src, const int64_t* d_src_off, c
                                int32_t* d_status, int64_t n, lz4m_stream_t stream);
 
 /*
+ * Batched LZ4_decompress_safe_usingDict (lz4.c:2612-2625) with the
+ * dictionaries in a buffer laid out like d_dst: block i's dictionary is the
+ * d_dict_len[i] bytes ending at d_dict_base + d_dst_off[i].  Built for
+ * linked-block frames (LZ4F_decompress, lz4frame.c:1853-1856): the previous
+ * round's output of the whole frame as d_dict_base, so block i sees the
+ * last <= 64 KiB before its slot (lz4.frame's speculative rounds, DESIGN.md
+ * section 3.3).  One wavefront per block (the on-chip-history decoder);
+ * statuses and bytes are those of lz4m_decompress_batch_dict with the same
+ * dictionaries.  The call must not write the dictionary bytes (d_dict_base
+ * != d_dst unless the dictionaries lie outside every output slot).
+ */
+int lz4m_decompress_batch_prefix(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len,
+                                 uint8_t* d_dst, const int64_t* d_dst_off, const int32_t* d_dst_cap,
+                                 const uint8_t* d_dict_base, const int32_t* d_dict_len, int32_t* d_status, int64_t n,
+                                 lz4m_stream_t stream);
+
+/*
  * Linked-block frame decode (LZ4F_decompress on a blockLinked frame,
  * lz4frame.c:1844-1856): block i may reference the output of blocks < i, so
  * blocks decode in order on one wavefront, contiguously into d_dst (capacity

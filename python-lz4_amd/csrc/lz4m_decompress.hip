@@ -966,8 +966,12 @@ __device__ __forceinline__ CoopSeq coop_parse(const lds_u8* IN, int32_t t, u32x4
 // long copies on the whole wave (as decompress_chain_kernel); returns the
 // reference's result (decoded size or -(error position)-1).  Output [0, op)
 // must already be in HBM and visible to the wave.
+// DICT: the dlen bytes before dict_end are the block's dictionary
+// (LZ4_decompress_safe_usingDict, as decompress_kernel<true>).
+template <bool DICT = false>
 __device__ __forceinline__ int32_t coop_finish(const uint8_t* s, uint8_t* d, int32_t iend, int32_t oend, int32_t ip,
-                                               int32_t op, bool fast, uint32_t lane) {
+                                               int32_t op, bool fast, uint32_t lane, int32_t dlen = 0,
+                                               const uint8_t* dict_end = nullptr) {
     Lane L;
     L.live = false;
     L.result = -1;
@@ -978,14 +982,14 @@ __device__ __forceinline__ int32_t coop_finish(const uint8_t* s, uint8_t* d, int
         L.oend = oend;
         L.ip = ip;
         L.op = op;
-        L.dict_len = 0;
-        L.dict_end = d;
+        L.dict_len = DICT ? dlen : 0;
+        L.dict_end = DICT ? dict_end : d;
         L.fast = fast;
         L.live = true;
     }
     while (__any(L.live)) {
         Copy lc{kNone, 0, 0, 0}, mc{kNone, 0, 0, 0};
-        if (L.live) decode_step<false, false>(L, lc, mc);
+        if (L.live) decode_step<DICT, false>(L, lc, mc);
         if (__ballot(lc.kind != kNone || mc.kind != kNone) == 0) continue;
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
         const int64_t oe = readlane64(L.oend, 0);
@@ -997,7 +1001,11 @@ __device__ __forceinline__ int32_t coop_finish(const uint8_t* s, uint8_t* d, int
         }
         if (__builtin_amdgcn_readlane(mc.kind, 0) != kNone) {
             const int64_t dp = readlane64(mc.dpos, 0), mo = readlane64(mc.arg, 0), ln = readlane64(mc.len, 0);
-            wave_match(d + dp, mo, ln, oe - dp, lane);
+            if (DICT && mo < 0) {   // starts in the dictionary (the chain kernel's convention)
+                if (lane == 0) dict_match(L, dp, -mo, ln);
+            } else {
+                wave_match(d + dp, mo, ln, oe - dp, lane);
+            }
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
         }
     }
@@ -1212,12 +1220,21 @@ __device__ unsigned long long g_hist_prof[16];
 #define HP_FLUSH() do {} while (0)
 #endif
 
+// DICT (linked frames, lz4m_decompress_batch_prefix): block b's dictionary
+// is the dict_len[b] bytes ending at d + ddelta, where d is its output slot
+// (ddelta = the distance from the output buffer to an equally laid-out
+// dictionary buffer: the previous round of a linked frame).  A match whose
+// whole source lies in the dictionary takes the parallel path (its bytes are
+// read from there); anything else that reaches before the block goes to the
+// exact state machine with the same dictionary (decode_step<true>).
+template <bool DICT>
 __global__ __launch_bounds__(256, 4) void hist_decompress_kernel(const uint8_t* __restrict__ src,
                                                                  const int64_t* __restrict__ src_off,
                                                                  const int32_t* __restrict__ src_len, uint8_t* dst,
                                                                  const int64_t* __restrict__ dst_off,
                                                                  const int32_t* __restrict__ dst_cap,
-                                                                 int32_t* __restrict__ status, int64_t n) {
+                                                                 int32_t* __restrict__ status, int64_t n,
+                                                                 const int32_t* __restrict__ dict_len, int64_t ddelta) {
     __shared__ __attribute__((aligned(16))) uint8_t ins[4][kCoopIn + 64];
     __shared__ __attribute__((aligned(16))) uint8_t outs[4][kHistW + 32];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -1233,6 +1250,7 @@ __global__ __launch_bounds__(256, 4) void hist_decompress_kernel(const uint8_t* 
             continue;
         }
         const bool fast = oend >= 64;
+        const int32_t dlen = DICT ? dict_len[b] : 0;
         int32_t ip = 0, op = 0, base = 0, F = 0, ib = -kCoopIn;
         bool fit_cut = false;   // the last round stopped at a sequence that only did not fit the buffer
         HP_MARK(15);
@@ -1367,8 +1385,10 @@ __global__ __launch_bounds__(256, 4) void hist_decompress_kernel(const uint8_t* 
             // the reference's fast-loop margins (lz4.c:2004-2110, as fast_seq / decode_step)
             const bool lit_ok = q.litx ? ib + q.litpos + lit <= iend - 32 && o + lit <= oend - 32
                                        : sabs + 1 <= iend - 17;
+            // DICT: a source entirely in the dictionary
+            const bool in_dict = DICT && off > o + lit && off <= o + lit + dlen && off >= 16 && o + lit - off + ml <= 0;
             const bool ok_nofit = act && q.simple && lit_ok && (!q.mlx || sabs + adv <= iend - 4) && off >= 1 &&
-                                  off <= o + lit && o + len < oend - 64;
+                                  (off <= o + lit || in_dict) && o + len < oend - 64;
             const bool ok = ok_nofit && o + len <= base + kHistW;
             const uint64_t bad = __ballot(act) & ~__ballot(ok);
             const int use = bad ? __builtin_ctzll(bad) : nseq;
@@ -1386,7 +1406,7 @@ __global__ __launch_bounds__(256, 4) void hist_decompress_kernel(const uint8_t* 
             // so the HBM round trip overlaps the literal phase
             const bool far = u && m - off < base;
             u32x4 pre = u32x4{0, 0, 0, 0};
-            if (far) pre = ld16(d + (m - off));
+            if (far) pre = ld16(d + (m - off) + (DICT && m - off < 0 ? ddelta : 0));
             if (u && lit > 0) {
                 if (lit <= 12) {
                     lds_put_exact(OB + (o - base), window_shift1(w), lit);
@@ -1421,7 +1441,9 @@ __global__ __launch_bounds__(256, 4) void hist_decompress_kernel(const uint8_t* 
                     if (off >= 16) {
                         for (int32_t i = 0; i < ml; i += 16) {
                             const int32_t sp = s0 + i;   // < base: flushed long ago (base <= F - 4 K)
-                            const u32x4 v = (i == 0 && far) ? pre : sp >= base ? lds_ld16(OB + (sp - base)) : ld16(d + sp);
+                            const u32x4 v = (i == 0 && far)   ? pre
+                                            : sp >= base          ? lds_ld16(OB + (sp - base))
+                                                                  : ld16(d + sp + (DICT && sp < 0 ? ddelta : 0));
                             lds_put_exact(OB + (m - base + i), v, ml - i);
                         }
                     } else {   // s0 > m - 16 >= base
@@ -1448,7 +1470,7 @@ __global__ __launch_bounds__(256, 4) void hist_decompress_kernel(const uint8_t* 
         for (int32_t c = F + 16 * (int32_t)lane; c < op; c += 16 * kWave)
             coop_put(d + c, lds_ld16(OB + (c - base)), op - c);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-        const int32_t r = coop_finish(s, d, iend, oend, ip, op, fast, lane);
+        const int32_t r = coop_finish<DICT>(s, d, iend, oend, ip, op, fast, lane, dlen, d + ddelta);
         if (lane == 0) status[b] = r;
         HP_MARK(7);
         HP_COUNT(11, 1);
@@ -1644,8 +1666,8 @@ extern "C" int lz4m_decompress_batch_sel(const uint8_t* d_src, const int64_t* d_
         const int64_t grid = (n + 3) / 4;
         const dim3 g((uint32_t)(grid < 65536 ? grid : 65536));
         if (decoder == kHistDec)   // the on-chip-history kernel; kCoopDec: the HBM-only one (A/B)
-            hipLaunchKernelGGL(hist_decompress_kernel, g, dim3(256), 0, st, d_src, d_src_off, d_src_len, d_dst,
-                               d_dst_off, d_dst_cap, d_status, n);
+            hipLaunchKernelGGL(hist_decompress_kernel<false>, g, dim3(256), 0, st, d_src, d_src_off, d_src_len, d_dst,
+                               d_dst_off, d_dst_cap, d_status, n, nullptr, (int64_t)0);
         else
             hipLaunchKernelGGL(coop_decompress_kernel, g, dim3(256), 0, st, d_src, d_src_off, d_src_len, d_dst,
                                d_dst_off, d_dst_cap, d_status, n);
@@ -1696,6 +1718,20 @@ extern "C" int lz4m_decompress_batch_dict(const uint8_t* d_src, const int64_t* d
     hipLaunchKernelGGL(decompress_kernel<true>, dim3((uint32_t)grid), dim3(256), 0, (hipStream_t)stream, d_src,
                        d_src_off, d_src_len, d_dst, d_dst_off, d_dst_cap, d_dict, d_dict_off, d_dict_len, d_status,
                        n, nullptr);
+    return (int)hipGetLastError();
+}
+
+extern "C" int lz4m_decompress_batch_prefix(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len,
+                                            uint8_t* d_dst, const int64_t* d_dst_off, const int32_t* d_dst_cap,
+                                            const uint8_t* d_dict_base, const int32_t* d_dict_len,
+                                            int32_t* d_status, int64_t n, lz4m_stream_t stream) {
+    if (n < 0 || (n > 0 && d_dict_base == nullptr)) return LZ4M_EINVAL;
+    if (n == 0) return 0;
+    const int64_t grid = (n + 3) / 4;
+    const int64_t delta = (int64_t)((intptr_t)d_dict_base - (intptr_t)d_dst);
+    hipLaunchKernelGGL(hist_decompress_kernel<true>, dim3((uint32_t)(grid < 65536 ? grid : 65536)), dim3(256), 0,
+                       (hipStream_t)stream, d_src, d_src_off, d_src_len, d_dst, d_dst_off, d_dst_cap, d_status, n,
+                       d_dict_len, delta);
     return (int)hipGetLastError();
 }
 

@@ -48,6 +48,7 @@ def _declare(lib) -> None:
         "lz4m_decompress_workspace_size": ([i64, i64], C.c_size_t),
         "lz4m_decompress_batch_sel": ([vp, vp, vp, vp, vp, vp, vp, i64, vp, C.c_size_t, i32, vp], i32),
         "lz4m_decompress_batch_dict": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, vp], i32),
+        "lz4m_decompress_batch_prefix": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, vp], i32),
         "lz4m_decompress_chain": ([vp, vp, vp, vp, vp, vp, i64, i32, vp], i32),
         "lz4m_compress_batch": ([vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, vp], i32),
         "lz4m_compress_dict_batch": ([vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, vp], i32),
@@ -160,6 +161,17 @@ def release_workspaces() -> None:
     """Drop the cached decoder scratch (it grows to ~1/3 of the largest
     compressed batch decoded)."""
     _WORK.clear()
+
+
+def launch_decompress_prefix(src, src_off, src_len, dst, dst_off, dst_cap, dict_base, dict_len, status, n,
+                             stream=None) -> None:
+    """Batched LZ4_decompress_safe_usingDict, block i's dictionary the
+    dict_len[i] bytes ending at offset dst_off[i] of ``dict_base`` (laid out
+    like ``dst``; lz4m_decompress_batch_prefix)."""
+    check(lib().lz4m_decompress_batch_prefix(ptr(src), ptr(src_off), ptr(src_len), ptr(dst), ptr(dst_off),
+                                             ptr(dst_cap), ptr(dict_base), ptr(dict_len), ptr(status), n,
+                                             stream_ptr(stream)),
+          "lz4m_decompress_batch_prefix")
 
 
 def launch_decompress_chain(src, src_off, src_len, raw_mask, dst, status, n, max_block, stream=None) -> None:

@@ -522,12 +522,16 @@ def _decode_linked(d_frame, c_off, c_len, raw_mask, out, status, maxb):
     round's output as its dictionary (two buffers), until a round changes no
     byte and no status.  At that fixed point block k was decoded with the
     true output of block k-1 and, by induction from block 0 (no dictionary),
-    every block equals the serial chain's.  This needs every block but the
-    last to decode to exactly the block size (what LZ4F_compressFrame and the
-    lz4 tool write); otherwise, or with LZ4M_LINKED_DECODE=serial, blocks
-    decode in order on one wavefront (lz4m_decompress_chain)."""
+    every block equals the serial chain's.  A round is one launch of the
+    one-wavefront-per-block decoder with the other buffer as dictionary
+    (lz4m_decompress_batch_prefix; LZ4M_LINKED_DECODE=dict: the lane-per-
+    block dictionary kernel).  This needs every block but the last to decode
+    to exactly the block size (what LZ4F_compressFrame and the lz4 tool
+    write); otherwise, or with LZ4M_LINKED_DECODE=serial, blocks decode in
+    order on one wavefront (lz4m_decompress_chain)."""
     nb = c_off.numel()
-    if nb <= 2 or os.environ.get("LZ4M_LINKED_DECODE", "") == "serial":
+    mode = os.environ.get("LZ4M_LINKED_DECODE", "")
+    if nb <= 2 or mode == "serial":
         N.launch_decompress_chain(d_frame, c_off, c_len, raw_mask, out, status, nb, maxb)
         return
     dev = d_frame.device
@@ -547,18 +551,28 @@ def _decode_linked(d_frame, c_off, c_len, raw_mask, out, status, maxb):
     cur = 0
     for r in range(nb + 1):
         prev = cur ^ 1
-        N.launch_decompress(d_frame, c_off, dec_len, bufs[cur], slot_off, caps, sts[cur], nb,
-                            dict_buf=bufs[prev], dict_off=dict_off, dict_len=dlen)
+        if mode == "dict":
+            N.launch_decompress(d_frame, c_off, dec_len, bufs[cur], slot_off, caps, sts[cur], nb,
+                                dict_buf=bufs[prev], dict_off=dict_off, dict_len=dlen)
+        else:
+            N.launch_decompress_prefix(d_frame, c_off, dec_len, bufs[cur], slot_off, caps, bufs[prev], dlen,
+                                       sts[cur], nb)
         sts[cur] = torch.where(raw_mask, c_len, sts[cur])
         if r > 0 and torch.equal(sts[cur], sts[prev]) and torch.equal(bufs[cur][:span], bufs[prev][:span]):
             break
         cur = prev
-    st = sts[cur]
+    if bufs[cur] is not out:
+        out[:span].copy_(bufs[cur][:span])
+    _linked_status(d_frame, c_off, c_len, raw_mask, out, status, nb, maxb, sts[cur])
+
+
+def _linked_status(d_frame, c_off, c_len, raw_mask, out, status, nb, maxb, st):
+    """Accept the speculative result unless a block before the first failing
+    one decoded short of the block size (then the blocks' positions differ
+    from the slots: the serial chain decodes the frame instead)."""
     bad = st < 0
     upto = int(torch.nonzero(bad).flatten()[0]) if bool(bad.any()) else nb - 1
     if upto > 0 and not bool((st[:upto] == maxb).all()):       # a short block mid-frame: positions differ
         N.launch_decompress_chain(d_frame, c_off, c_len, raw_mask, out, status, nb, maxb)
         return
-    if bufs[cur] is not out:
-        out[:span].copy_(bufs[cur][:span])
     status.copy_(st)

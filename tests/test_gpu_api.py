@@ -338,14 +338,20 @@ def _frame_bytes(blocks, linked=True, bsid=4):
     return out + struct.pack("<I", 0)
 
 
-@pytest.mark.parametrize("mode", ["speculative", "serial"])
+@pytest.mark.parametrize("mode", ["speculative", "dict", "serial"])
 def test_frame_linked_decode_modes(gpu, reference, monkeypatch, mode):
-    """Linked frames decode identically whichever way: speculative rounds
-    (every block but the last full) and the serial chain -- including a frame
-    whose stored short block mid-stream forces the serial path."""
+    """Linked frames decode identically whichever way: speculative rounds in
+    place on the prefix decoder (default) or double-buffered on the dictionary
+    kernel, and the serial chain -- including a frame whose stored short
+    block mid-stream forces the serial path, and a 96-block default frame of
+    mixed kinds (several speculative rounds)."""
     from lz4 import _synth
-    if mode == "serial":
-        monkeypatch.setenv("LZ4M_LINKED_DECODE", "serial")
+    if mode != "speculative":
+        monkeypatch.setenv("LZ4M_LINKED_DECODE", mode)
+    mixed = b"".join(_synth.blocks(16, k, seed=23).tobytes()
+                     for k in ("text", "silesia", "markup", "random", "records", "runs"))
+    fm = lz4.frame.compress(mixed)   # the default: 64 KiB linked blocks, byte-identical to the reference
+    assert lz4.frame.decompress(fm) == mixed
     data = b"".join(_synth.blocks(3, k, seed=19).tobytes() for k in ("silesia", "text", "records", "runs"))
     for bs in (4, 5):
         f = lz4.frame.compress(data, block_size=bs, block_linked=True)

@@ -427,3 +427,65 @@ def test_decompress_high_ratio(gpu, oracle, decoder, block):
     got = gpu_decompress(comp, [block] * len(blocks), gpu, decoder)
     for (st, out), b in zip(got, blocks):
         assert st == len(b) and out == b
+
+
+def test_decompress_prefix_matches_oracle(gpu, oracle, corpus):
+    """lz4m_decompress_batch_prefix (the linked-frame decoder: each block's
+    dictionary ends where its slot starts, in a second buffer laid out like
+    the output) against the oracle's
+    LZ4_decompress_safe_usingDict (lz4.c:2612-2625), on blocks compressed
+    against dictionaries of 0 B .. 64 KiB, mutated / truncated copies and
+    capacities around the true size; nothing outside a slot is written."""
+    blocks, _ = corpus
+    rng = random.Random(77)
+    cases = []
+    for i in range(700):
+        b = blocks[rng.randrange(len(blocks))]
+        dl = rng.choice([0, 5, 16, 100, 5000, 30000, 65536])
+        n = rng.choice([100, 2000, 20000, 65536 - dl if dl < 65536 else 65536])
+        n = max(1, min(n, 65536))
+        joined = b + blocks[rng.randrange(len(blocks))]
+        start = rng.randrange(0, len(joined) - (dl + n) + 1) if len(joined) >= dl + n else 0
+        dic, data = joined[start:start + dl], joined[start + dl:start + dl + n]
+        c = bytearray(oracle.compress_dict(data, dic) if dl >= 8 else oracle.compress(data))
+        if i % 3 == 1:
+            for _ in range(rng.randrange(1, 4)):
+                c[rng.randrange(len(c))] = rng.randrange(256)
+        if i % 7 == 2:
+            c = c[:rng.randrange(len(c) + 1)]
+        cap = rng.choice([len(data), len(data), len(data) - 1, len(data) + 77, max(0, len(data) - 9)])
+        cases.append((dic, bytes(c), cap, len(data)))
+    # two buffers laid out alike: the output [gap][slot_i (cap_i)][64-byte guard] ..., and the
+    # dictionaries, dict_i ending where slot_i starts (the output's gaps hold a sentinel)
+    out_b, dic_b, doff, dl, caps = bytearray(), bytearray(), [], [], []
+    for dic, c, cap, _ in cases:
+        out_b += b"\x5A" * len(dic)
+        dic_b += dic
+        doff.append(len(out_b))
+        dl.append(len(dic))
+        caps.append(cap)
+        out_b += b"\xA5" * (cap + 64)
+        dic_b += b"\x00" * (cap + 64)
+    packed, offs, lens = _pack([c for _, c, _, _ in cases])
+    dev = gpu
+    d_src = torch.frombuffer(bytearray(packed), dtype=torch.uint8).to(dev)
+    d_out = torch.frombuffer(bytearray(out_b), dtype=torch.uint8).to(dev)
+    d_dic = torch.frombuffer(bytearray(dic_b), dtype=torch.uint8).to(dev)
+    so = torch.tensor(offs, dtype=torch.int64, device=dev)
+    sl = torch.tensor(lens, dtype=torch.int32, device=dev)
+    do = torch.tensor(doff, dtype=torch.int64, device=dev)
+    dc = torch.tensor(caps, dtype=torch.int32, device=dev)
+    dd = torch.tensor(dl, dtype=torch.int32, device=dev)
+    st = torch.empty(len(cases), dtype=torch.int32, device=dev)
+    N.launch_decompress_prefix(d_src, so, sl, d_out, do, dc, d_dic, dd, st, len(cases))
+    torch.cuda.synchronize()
+    out, status = bytes(d_out.cpu().numpy()), st.cpu().tolist()
+    assert bytes(d_dic.cpu().numpy()) == bytes(dic_b), "the dictionary buffer was written"
+    for i, (dic, c, cap, n) in enumerate(cases):
+        want_s, want = oracle.decompress(c, cap, dict_=dic if dic else None)
+        assert status[i] == want_s, (i, len(dic), cap, status[i], want_s)
+        o = doff[i]
+        if want_s >= 0:
+            assert out[o:o + want_s] == want, i
+        assert out[o + cap:o + cap + 64] == b"\xA5" * 64, ("wrote past the slot", i)
+        assert out[o - len(dic):o] == b"\x5A" * len(dic), ("wrote before the slot", i)
