@@ -222,6 +222,15 @@ def compress_device(d_src: torch.Tensor, n: int | None = None, *, compression_le
                            block_linked=block_linked, store_size=store_size, parse=parse, stream=stream)[0]
 
 
+def _host_wait(stream) -> None:
+    """Block until `stream` drains, with the GIL released (an event wait;
+    tensor.item() waits holding the GIL, so a host hashing thread would sit
+    idle for the whole device phase)."""
+    ev = torch.cuda.Event()
+    ev.record(stream)
+    ev.synchronize()
+
+
 def _compress_frame(d_src, n=None, *, compression_level=0, block_size=0, content_checksum=False,
                     block_checksum=False, block_linked=True, store_size=True, parse="exact", stream=None,
                     host_src=None):
@@ -291,6 +300,8 @@ def _compress_frame(d_src, n=None, *, compression_level=0, block_size=0, content
         rec_len = torch.empty(nb, dtype=torch.int32, device=dev)
         N.frame_block_sizes(raw_len, cmp_len, block_checksum, rec_len, nb, stream)
         frame_off = N.exclusive_scan(rec_len, stream=stream)
+        if hthread is not None:   # wait with the GIL released: .item() waits holding it, stalling the hash thread
+            _host_wait(main)
         total = int(frame_off[-1].item())
     tail = 4 + (4 if content_checksum else 0)
     out = torch.empty(len(hdr) + total + tail + 16, dtype=torch.uint8, device=dev)
