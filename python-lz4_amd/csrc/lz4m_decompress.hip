@@ -301,15 +301,29 @@ __device__ __forceinline__ void lane_match(uint8_t* d, int64_t off, int64_t len,
 
 // ---------------------------------------------------------- wave copies
 // All 64 lanes execute the same copy (uniform arguments).
+// Literal bytes never overlap their destination, so each lane requests four
+// 16-byte pieces before storing any: a long literal (a stored-looking block's
+// 64 KiB) waits on one memory round trip per 4 KiB instead of per 1 KiB.
 __device__ __forceinline__ void wave_literal(uint8_t* d, const uint8_t* s, int64_t len, int64_t d_room,
                                              int64_t s_room, uint32_t lane) {
-    for (int64_t base = 0; base < len; base += 16 * kWave) {
-        const int64_t pos = base + 16 * (int64_t)lane;
-        if (pos < len) {
-            if (len - pos >= 16 || (d_room - pos >= 16 && s_room - pos >= 16)) {
-                st16(d + pos, ld16(s + pos));
-            } else {
-                for (int64_t k = pos; k < len; ++k) d[k] = s[k];
+    constexpr int kU = 4;
+    for (int64_t base = 0; base < len; base += 16 * kWave * kU) {
+        u32x4 v[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int64_t pos = base + 16 * kWave * u + 16 * (int64_t)lane;
+            const bool whole = pos < len && (len - pos >= 16 || s_room - pos >= 16);
+            v[u] = whole ? ld16(s + pos) : u32x4{0, 0, 0, 0};
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int64_t pos = base + 16 * kWave * u + 16 * (int64_t)lane;
+            if (pos < len) {
+                if (len - pos >= 16 || (d_room - pos >= 16 && s_room - pos >= 16)) {
+                    st16(d + pos, v[u]);
+                } else {
+                    for (int64_t k = pos; k < len; ++k) d[k] = s[k];
+                }
             }
         }
     }
@@ -887,9 +901,19 @@ __device__ __forceinline__ int32_t coop_incl_sum(int32_t v) {
 // Exact-length whole-wave copies (no wild bytes: other sequences' output may
 // already sit right after them).
 __device__ __forceinline__ void coop_copy_literal(uint8_t* d, const uint8_t* s, int32_t len, uint32_t lane) {
-    for (int32_t base = 0; base < len; base += 16 * kWave) {
-        const int32_t pos = base + 16 * (int32_t)lane;
-        if (pos < len) coop_put(d + pos, ld16(s + pos), len - pos);
+    constexpr int kU = 4;   // four pieces requested before any is stored (as wave_literal)
+    for (int32_t base = 0; base < len; base += 16 * kWave * kU) {
+        u32x4 v[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int32_t pos = base + 16 * kWave * u + 16 * (int32_t)lane;
+            v[u] = pos < len ? ld16(s + pos) : u32x4{0, 0, 0, 0};
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int32_t pos = base + 16 * kWave * u + 16 * (int32_t)lane;
+            if (pos < len) coop_put(d + pos, v[u], len - pos);
+        }
     }
 }
 
@@ -1641,7 +1665,7 @@ extern "C" int lz4m_decompress_batch_sel(const uint8_t* d_src, const int64_t* d_
     // sequence lengths (lz4m_decompress_workspace_size)
     const bool rows_fit = work_bytes >= lz4m_rows_fixed_bytes(n) + 64;
     // LZ4M_ROWS_MIN_BLOCKS: smallest batch sent to the row decoder (tuning)
-    static const int rows_min = env_int("LZ4M_ROWS_MIN_BLOCKS", 98305);
+    static const int rows_min = env_int("LZ4M_ROWS_MIN_BLOCKS", 32768);   // crossover measured, DESIGN 3.1
     // LZ4M_COOP_MAX_BLOCKS: largest batch sent to the one-wave-per-block decoder
     static const int coop_max = env_int("LZ4M_COOP_MAX_BLOCKS", 98304);
     if (decoder == kAuto) {

@@ -469,9 +469,9 @@ def decompress_host(comp: torch.Tensor, comp_off: torch.Tensor, comp_len: torch.
     the copies to overlap); comp_off / out_off int64, comp_len / out_cap
     int32 host tensors, blocks in increasing position order in both.
     Returns the int32 status of every block (host), as LZ4_decompress_safe
-    would return it.  The default 64 K-block chunks run the one-wave-per-
-    block (hist) decoder; chunks above 98 304 blocks the large-batch row
-    decoder (lz4m_decompress_batch_sel's switch-over, DESIGN.md section 3)."""
+    would return it.  Chunks of 32 768 blocks or more (the default 65 536)
+    run the large-batch row decoder, smaller ones the one-wave-per-block
+    decoder (lz4m_decompress_batch_sel's switch-over, DESIGN.md section 3.1)."""
     dev = device or N.device()
     n = comp_off.numel()
     status = torch.empty(n, dtype=torch.int32, device=dev)

@@ -317,7 +317,7 @@ def _offset0_block(lit, ml):
 
 @pytest.mark.parametrize("decoder", ["auto", "lane"])
 def test_decompress_large_batch_edges(gpu, oracle, corpus, decoder):
-    """A batch above the small-batch switch-over (98 304 blocks), so the
+    """A batch above the small-batch switch-over (32 768 blocks), so the
     default dispatch runs the large-batch decoder, with every edge case of the
     small tests embedded: the golden decode vectors with their capacities,
     3 000 mutated / truncated blocks, random garbage, ragged sizes 0..65536,
