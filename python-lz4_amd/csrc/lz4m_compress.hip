@@ -23,6 +23,8 @@
 // by lane 0.
 #include "lz4m_common.h"
 
+#include <type_traits>
+
 #include <stdio.h>
 #include <stdlib.h>
 #include "../../include/lz4m.h"
@@ -55,16 +57,24 @@ constexpr int kMaxInput = 0x7E000000; // lz4.h:211
 __device__ __forceinline__ int64_t bound64(int64_t n) { return n + n / 255 + 16; }
 
 // F(m) = sum_{j=0..m} floor(j/64), m >= -1
-__device__ __forceinline__ int64_t skip_sum(int64_t m) {
-    if (m < 0) return 0;
-    const int64_t q = m >> 6, r = m & 63;
+template <typename I = int64_t>
+__device__ __forceinline__ I skip_sum(I m) {
+    if constexpr (std::is_signed<I>::value)
+        if (m < 0) return 0;
+    const I q = m >> 6, r = m & 63;
     return 32 * q * (q - 1) + q * (r + 1);
 }
 
 // offset from ip of search attempt k (lz4.c:1021-1027: step = attempts++ >> 6)
-__device__ __forceinline__ int64_t attempt_off(int64_t k, int64_t A, int64_t FA) {
-    return k >= 1 ? 1 + skip_sum(A + k - 2) - FA : 0;
+template <typename I = int64_t>
+__device__ __forceinline__ I attempt_off(I k, I A, I FA) {
+    return k >= 1 ? 1 + skip_sum<I>(A + k - 2) - FA : 0;
 }
+
+// Acceleration 1 (every python-lz4 default) keeps the search schedule in
+// 32-bit unsigned registers (A = 64, FA = 0): a search stops at the first
+// step that passes mflimit, so the largest offset it computes is below
+// n + 2^20 < 2^32 for any n <= LZ4_MAX_INPUT_SIZE.
 
 typedef __attribute__((address_space(3))) uint16_t lds_t16;   // hash-table entries in LDS
 typedef __attribute__((address_space(3))) uint32_t lds_t32;
@@ -321,7 +331,7 @@ __device__ __forceinline__ u32x4 readlane_x4(u32x4 v, int l) {
 // (zeroed for a fresh stream, lz4.c:1513 / LZ4_prepareTable; loaded from a
 // dictionary; or carried over from the previous block).
 // oracle: orc_compress_window (oracle/lz4_oracle.c).
-template <int V>
+template <int V, bool ACC1 = false>
 __device__ __forceinline__ int32_t compress_block_w(const uint8_t* __restrict__ w, int32_t hist, int32_t n, uint8_t* dst,
                                     int32_t cap, int accel, uint16_t* tab, lds_u8* ring, uint32_t lane,
                                     uint32_t ibase, uint32_t low_idx, int32_t low_src, int32_t low_dict) {
@@ -338,8 +348,9 @@ __device__ __forceinline__ int32_t compress_block_w(const uint8_t* __restrict__ 
     const int32_t iend = hist + n;
     const int32_t mflimit1 = iend - 12 + 1;                     // lz4.c:942
     const int32_t matchlimit = iend - 5;
-    const int64_t A = (int64_t)accel << 6;                      // searchMatchNb start
-    const int64_t FA = skip_sum(A - 1);
+    using SI = typename std::conditional<ACC1, uint32_t, int64_t>::type;   // search-schedule integers
+    const SI A = ACC1 ? (SI)64 : (SI)((int64_t)accel << 6);   // searchMatchNb start
+    const SI FA = ACC1 ? (SI)0 : skip_sum<SI>(A - 1);
     int32_t anchor = hist, ip = hist, op = 0;
     Win W{ring, hist, hist, iend};
     // the match being encoded: ip side P = [pbase, pbase+16), candidate side
@@ -360,14 +371,14 @@ __device__ __forceinline__ int32_t compress_block_w(const uint8_t* __restrict__ 
         uint32_t tok_hi;   // literal-length nibble; the token byte is written once, with the match nibble
         uint32_t PM, GM;
         {   // ---- search (lz4.c:1016-1075), 64 attempts per wave step ----
-            int64_t k0 = 0;
+            SI k0 = 0;
             for (;;) {
-                const int64_t k = k0 + lane;
+                const SI k = k0 + (SI)lane;
                 // attempts 0..63 of acceleration 1 are consecutive positions
                 const bool unit = A == 64 && k0 == 0;
-                const int64_t pos64 = ip + (unit ? k : attempt_off(k, A, FA));
-                const int64_t nxt = unit ? pos64 + 1 : ip + 1 + skip_sum(A + k - 1) - FA;   // attempt k+1
-                const bool valid = nxt <= mflimit1;
+                const SI pos64 = ip + (unit ? k : attempt_off<SI>(k, A, FA));
+                const SI nxt = unit ? pos64 + 1 : ip + 1 + skip_sum<SI>(A + k - 1) - FA;   // attempt k+1
+                const bool valid = nxt <= (SI)mflimit1;
                 const int32_t pos = valid ? (int32_t)pos64 : ip;
                 const uint64_t vmask = __ballot(valid);
                 const int nvalid = __builtin_popcountll(vmask);   // valid lanes are a prefix
@@ -412,7 +423,7 @@ __device__ __forceinline__ int32_t compress_block_w(const uint8_t* __restrict__ 
                 CP_MARK(1);
                 // the serial loop inserted an earlier lane of the group first
                 const uint32_t cand =
-                    pred >= 0 ? ibase + (uint32_t)(ip + (unit ? (int64_t)pred : attempt_off(k0 + pred, A, FA))) : old;
+                    pred >= 0 ? ibase + (uint32_t)(ip + (unit ? (SI)pred : attempt_off<SI>(k0 + pred, A, FA))) : old;
                 int32_t cpos = pos;
                 bool ok = false;
                 u32x4 gv = u32x4{0, 0, 0, 0};
@@ -644,19 +655,20 @@ __device__ __forceinline__ void zero_table(uint16_t* tab, uint32_t lane) {
 }
 
 // One block with a fresh table (LZ4_compress_generic_validated, noDict).
-template <int V>
+template <int V, bool ACC1>
 __device__ __forceinline__ int64_t compress_block(const uint8_t* __restrict__ src, int64_t n, uint8_t* dst,
                                                   int64_t cap, int accel, uint16_t* tab, lds_u8* ring,
                                                   uint32_t lane) {
     if (n > kMaxInput) return 0;
     zero_table(tab, lane);
-    return compress_block_w<V>(src, 0, n, dst, cap, accel, tab, ring, lane, 0u, 0u, 0, 0);
+    return compress_block_w<V, ACC1>(src, 0, n, dst, cap, accel, tab, ring, lane, 0u, 0u, 0, 0);
 }
 
 // `only`: -1 every block; 0 only blocks < 65547 B; 1 only blocks >= 65547 B.
 // LZ4M_TABLE_AUTO launches the U16 kernel with 0 and the U32 kernel with 1
 // (lz4.c:1352-1357): one kernel holding both parses would need 196 VGPRs.
-template <int V>
+// ACC1: acceleration 1, the 32-bit search schedule (compress_block_w).
+template <int V, bool ACC1>
 __global__ __launch_bounds__(64) void compress_kernel(const uint8_t* __restrict__ src,
                                                       const int64_t* __restrict__ src_off,
                                                       const int32_t* __restrict__ src_len, uint8_t* dst,
@@ -669,7 +681,8 @@ __global__ __launch_bounds__(64) void compress_kernel(const uint8_t* __restrict_
     for (int64_t b = blockIdx.x; b < n; b += gridDim.x) {
         const int64_t len = src_len[b];
         if (only >= 0 && (len >= kLimit64K) != (only == 1)) continue;
-        const int64_t r = compress_block<V>(src + src_off[b], len, dst + dst_off[b], dst_cap[b], accel, tab, ring, lane);
+        const int64_t r = compress_block<V, ACC1>(src + src_off[b], len, dst + dst_off[b], dst_cap[b], accel, tab, ring,
+                                                  lane);
         if (lane == 0) out_len[b] = (int32_t)r;
     }
 }
@@ -877,14 +890,24 @@ extern "C" int lz4m_compress_batch(const uint8_t* d_src, const int64_t* d_src_of
     if (acceleration > 65537) acceleration = 65537;
     const uint32_t grid = (uint32_t)(n < (1ll << 30) ? n : (1ll << 30));
     hipStream_t s = (hipStream_t)stream;
+    // acceleration 1 (the python-lz4 default) runs the 32-bit-schedule instance
+    auto exact = [&](auto v_tag, int only) {
+        constexpr int V = decltype(v_tag)::value;
+        if (acceleration == 1)
+            hipLaunchKernelGGL((compress_kernel<V, true>), dim3(grid), dim3(64), 0, s, d_src, d_src_off, d_src_len, d_dst,
+                               d_dst_off, d_dst_cap, d_out_len, n, acceleration, only);
+        else
+            hipLaunchKernelGGL((compress_kernel<V, false>), dim3(grid), dim3(64), 0, s, d_src, d_src_off, d_src_len,
+                               d_dst, d_dst_off, d_dst_cap, d_out_len, n, acceleration, only);
+    };
+    using U16 = std::integral_constant<int, LZ4M_TABLE_U16_HASH4>;
+    using U32 = std::integral_constant<int, LZ4M_TABLE_U32_HASH5>;
     switch (table) {
         case LZ4M_TABLE_U16_HASH4:
-            hipLaunchKernelGGL(compress_kernel<LZ4M_TABLE_U16_HASH4>, dim3(grid), dim3(64), 0, s, d_src, d_src_off,
-                               d_src_len, d_dst, d_dst_off, d_dst_cap, d_out_len, n, acceleration, -1);
+            exact(U16{}, -1);
             break;
         case LZ4M_TABLE_U32_HASH5:
-            hipLaunchKernelGGL(compress_kernel<LZ4M_TABLE_U32_HASH5>, dim3(grid), dim3(64), 0, s, d_src, d_src_off,
-                               d_src_len, d_dst, d_dst_off, d_dst_cap, d_out_len, n, acceleration, -1);
+            exact(U32{}, -1);
             break;
         case LZ4M_PARSE_PARALLEL:
             return pcompress_launch(d_src, d_src_off, d_src_len, d_dst, d_dst_off, d_dst_cap, d_out_len, n, 0, s);
@@ -893,10 +916,8 @@ extern "C" int lz4m_compress_batch(const uint8_t* d_src, const int64_t* d_src_of
         case LZ4M_PARSE_PARALLEL_LARGE:
             return pcompress_launch(d_src, d_src_off, d_src_len, d_dst, d_dst_off, d_dst_cap, d_out_len, n, 2, s);
         case LZ4M_TABLE_AUTO:
-            hipLaunchKernelGGL(compress_kernel<LZ4M_TABLE_U16_HASH4>, dim3(grid), dim3(64), 0, s, d_src, d_src_off,
-                               d_src_len, d_dst, d_dst_off, d_dst_cap, d_out_len, n, acceleration, 0);
-            hipLaunchKernelGGL(compress_kernel<LZ4M_TABLE_U32_HASH5>, dim3(grid), dim3(64), 0, s, d_src, d_src_off,
-                               d_src_len, d_dst, d_dst_off, d_dst_cap, d_out_len, n, acceleration, 1);
+            exact(U16{}, 0);
+            exact(U32{}, 1);
             break;
         default:
             return LZ4M_EINVAL;
