@@ -376,6 +376,42 @@ template <bool STAGE>
 __device__ __forceinline__ bool read_len(const Lane& L, int64_t& ip, int64_t ilimit, bool initial_check,
                                          int64_t& out) {
     if (initial_check && ip >= ilimit) return false;
+    if (!STAGE) {
+        // 16 bytes per load: a run of 255s (a long literal or match, e.g. the
+        // 257 length bytes of a stored-looking 64 KiB block) costs one memory
+        // round trip per 16 bytes instead of per byte.  Same outcome as the
+        // byte loop below: reading the byte at ilimit fails with
+        // ip = ilimit + 1 (ilimit < iend, so every byte up to it is readable;
+        // ld16_guarded zero-fills past iend, i.e. past ilimit).
+        if (ip >= ilimit) {   // the first byte read already fails (ip + 1)
+            ++ip;
+            return false;
+        }
+        int64_t len = 0;
+        for (;;) {
+            const u32x4 v = ld16_guarded(L.src + ip, L.iend - ip);
+            const uint32_t n0 = ~v.x, n1 = ~v.y, n2 = ~v.z, n3 = ~v.w;
+            const uint32_t q = n0 ? 0u : n1 ? 1u : n2 ? 2u : n3 ? 3u : 4u;
+            if (q < 4) {
+                const uint32_t nw = q == 0 ? n0 : q == 1 ? n1 : q == 2 ? n2 : n3;
+                const uint32_t j = 4 * q + ((uint32_t)__builtin_ctz(nw) >> 3);   // first byte != 255
+                if (ip + (int64_t)j >= ilimit) {
+                    ip = ilimit + 1;
+                    return false;
+                }
+                len += 255 * (int64_t)j + (int64_t)byte_of(v, (int)j);
+                ip += j + 1;
+                out = len;
+                return true;
+            }
+            if (ip + 16 > ilimit) {   // the run reaches ilimit
+                ip = ilimit + 1;
+                return false;
+            }
+            len += 255 * 16;
+            ip += 16;
+        }
+    }
     int64_t len = 0;
     uint32_t s;
     do {
