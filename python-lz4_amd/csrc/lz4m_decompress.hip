@@ -304,9 +304,9 @@ __device__ __forceinline__ void lane_match(uint8_t* d, int64_t off, int64_t len,
 // Literal bytes never overlap their destination, so each lane requests four
 // 16-byte pieces before storing any: a long literal (a stored-looking block's
 // 64 KiB) waits on one memory round trip per 4 KiB instead of per 1 KiB.
+template <int kU = 4>   // pieces per lane per round trip (1 where registers are short: the stage kernel)
 __device__ __forceinline__ void wave_literal(uint8_t* d, const uint8_t* s, int64_t len, int64_t d_room,
                                              int64_t s_room, uint32_t lane) {
-    constexpr int kU = 4;
     for (int64_t base = 0; base < len; base += 16 * kWave * kU) {
         u32x4 v[kU];
 #pragma unroll
@@ -394,12 +394,13 @@ __device__ __forceinline__ bool read_len(const Lane& L, int64_t& ip, int64_t ili
             const uint32_t q = n0 ? 0u : n1 ? 1u : n2 ? 2u : n3 ? 3u : 4u;
             if (q < 4) {
                 const uint32_t nw = q == 0 ? n0 : q == 1 ? n1 : q == 2 ? n2 : n3;
-                const uint32_t j = 4 * q + ((uint32_t)__builtin_ctz(nw) >> 3);   // first byte != 255
+                const uint32_t bi = (uint32_t)__builtin_ctz(nw) >> 3;
+                const uint32_t j = 4 * q + bi;   // first byte != 255
                 if (ip + (int64_t)j >= ilimit) {
                     ip = ilimit + 1;
                     return false;
                 }
-                len += 255 * (int64_t)j + (int64_t)byte_of(v, (int)j);
+                len += 255 * (int64_t)j + (int64_t)((~nw >> (8 * bi)) & 0xFFu);   // no indexed access: no scratch
                 ip += j + 1;
                 out = len;
                 return true;
@@ -743,7 +744,7 @@ __device__ __forceinline__ void stage_coop(Lane& L, const Copy& c, uint32_t lane
             const uint8_t* s = readlane_ptr(L.src, l);
             const int64_t iend = readlane64(L.iend, l);
             const int64_t sp = readlane64(c.arg, l) + (a - readlane64(c.dpos, l));
-            wave_literal(d + a, s + sp, e - a, oend - a, iend - sp, lane);
+            wave_literal<1>(d + a, s + sp, e - a, oend - a, iend - sp, lane);
         } else {
             wave_match(d + a, readlane64(c.arg, l), e - a, oend - a, lane);
         }
@@ -1056,7 +1057,7 @@ __device__ __forceinline__ int32_t coop_finish(const uint8_t* s, uint8_t* d, int
         if (__builtin_amdgcn_readlane(lc.kind, 0) != kNone) {
             const int64_t ie = readlane64(L.iend, 0);
             const int64_t dp = readlane64(lc.dpos, 0), sp = readlane64(lc.arg, 0), ln = readlane64(lc.len, 0);
-            wave_literal(d + dp, s + sp, ln, oe - dp, ie - sp, lane);
+            wave_literal<DICT ? 1 : 4>(d + dp, s + sp, ln, oe - dp, ie - sp, lane);   // DICT: registers are short
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
         }
         if (__builtin_amdgcn_readlane(mc.kind, 0) != kNone) {
