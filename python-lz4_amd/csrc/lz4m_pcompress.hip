@@ -69,7 +69,11 @@ __device__ __forceinline__ uint64_t same_hash_mask(uint32_t h, bool act) {
     uint32_t lo = (uint32_t)a, hi = (uint32_t)(a >> 32);
 #pragma unroll
     for (int b = 0; b < HB; ++b) {
-        const uint32_t rep = (uint32_t)((int32_t)(h << (31 - b)) >> 31);   // bit b, replicated
+        // bit b, replicated, from one v_bfe_i32 that the ballot's compare
+        // also reads (written as plain C the compiler turns the compare into
+        // a shift + sign test: one VALU more per hash bit; measured +1.6 %)
+        uint32_t rep;
+        asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(rep) : "v"(h), "i"(b));
         const uint64_t B = __ballot(rep != 0u);
         // mask &= ~(B ^ rep) as one v_bitop3 per half: f(S0, S1, S2) =
         // S1 & (S0 xnor S2), truth table 0x84 (symmetric in S0 / S2)
@@ -142,16 +146,19 @@ __device__ __forceinline__ int32_t emit_seqs(const uint8_t* s, uint8_t* d, int32
     if (op + total > cap) return -1;
     for (int32_t t0 = 0; t0 < ptotal; t0 += 64) {
         const int32_t t = t0 + (int32_t)lane;
-        // last sequence k < ns with pbase_k <= t (pbase ascends with k)
-        int sq = 0;
+        // last sequence k < ns with pbase_k <= t (pbase ascends with k),
+        // searched in ds_bpermute byte-address units (4 k): each step's
+        // address is the previous one plus an instruction offset
+        int sq4 = 0;
 #pragma unroll
-        for (int step = 32; step > 0; step >>= 1) {
-            const int k = sq + step;
-            const int32_t pk = __shfl(pbase, k < ns ? k : 0);
-            if (k < ns && pk <= t) sq = k;
+        for (int step = 128; step >= 4; step >>= 1) {
+            const int k4 = sq4 + step;
+            const int32_t pk = __builtin_amdgcn_ds_bpermute(k4, pbase);
+            if (k4 < 4 * ns && pk <= t) sq4 = k4;
         }
-        const int32_t pb = __shfl(pbase, sq), ob = __shfl(obase, sq), L = __shfl(lit, sq), O = __shfl(off, sq),
-                      M = __shfl(ml, sq), S = __shfl(lstart, sq);
+        const int32_t pb = __builtin_amdgcn_ds_bpermute(sq4, pbase), ob = __builtin_amdgcn_ds_bpermute(sq4, obase),
+                      L = __builtin_amdgcn_ds_bpermute(sq4, lit), O = __builtin_amdgcn_ds_bpermute(sq4, off),
+                      M = __builtin_amdgcn_ds_bpermute(sq4, ml), S = __builtin_amdgcn_ds_bpermute(sq4, lstart);
         const int32_t EL = ext_len(L);
         const bool longlit = L >= kLongLit;
         int32_t r = t - pb;                 // index within the sequence's byte-parallel part
