@@ -83,7 +83,19 @@ __device__ __forceinline__ uint64_t same_hash_mask(uint32_t h, bool act) {
     return ((uint64_t)hi << 32) | lo;
 }
 
-__device__ __forceinline__ int32_t ext_len(int32_t x) { return x >= 15 ? 1 + (x - 15) / 255 : 0; }
+// y / 255 for y >= 0.  Blocks <= 64 KiB: (z + z/256) / 256 with z = y + 1,
+// exact for y < 65 790 (checked exhaustively), two shifts and two adds where
+// the division is a quarter-rate v_mul_hi_u32
+template <bool BIG>
+__device__ __forceinline__ int32_t div255(int32_t y) {
+    if (BIG) return y / 255;
+    const int32_t z = y + 1;
+    return (z + (z >> 8)) >> 8;
+}
+
+// length bytes after the token for a length field x (0 below 15)
+template <bool BIG>
+__device__ __forceinline__ int32_t ext_len(int32_t x) { return x >= 15 ? 1 + div255<BIG>(x - 15) : 0; }
 
 // inclusive prefix sum across the wave: row_shr 1/2/4/8 inside 16-lane rows,
 // then row_bcast:15 / row_bcast:31 carry the row totals (VALU only)
@@ -126,8 +138,9 @@ __device__ __forceinline__ int32_t wave_count(const uint8_t* s, int32_t a, int32
 // Encode `ns` sequences (lane s < ns holds lstart/lit/off/ml of sequence s;
 // ml == 0 marks the final literals-only sequence) at d + op, byte-parallel.
 // Returns the bytes written, or -1 if they do not fit before cap.
+template <bool BIG>
 __device__ __forceinline__ int32_t seq_size(int32_t lit, int32_t ml) {
-    return 1 + ext_len(lit) + lit + (ml ? 2 + ext_len(ml - 4) : 0);
+    return 1 + ext_len<BIG>(lit) + lit + (ml ? 2 + ext_len<BIG>(ml - 4) : 0);
 }
 
 constexpr int32_t kLongLit = 64;   // literals at least this long are copied 16 B per lane
@@ -139,6 +152,7 @@ constexpr int32_t kLongLit = 64;   // literals at least this long are copied 16 
 // copied by the whole wave, 16 bytes per lane).  Short-literal bytes come
 // from the registers of the current / previous 64-position chunk (v0 / vprev,
 // byte 0 of lane q - p0 is s[q]) when in reach, else from memory.
+template <bool BIG>
 __device__ __forceinline__ int32_t emit_seqs(const uint8_t* s, uint8_t* d, int32_t op, int32_t cap, int ns,
                                              int32_t lstart, int32_t lit, int32_t off, int32_t ml, int32_t obase,
                                              int32_t pbase, int32_t total, int32_t ptotal, int32_t p0, uint32_t v0,
@@ -159,7 +173,7 @@ __device__ __forceinline__ int32_t emit_seqs(const uint8_t* s, uint8_t* d, int32
         const int32_t pb = __builtin_amdgcn_ds_bpermute(sq4, pbase), ob = __builtin_amdgcn_ds_bpermute(sq4, obase),
                       L = __builtin_amdgcn_ds_bpermute(sq4, lit), O = __builtin_amdgcn_ds_bpermute(sq4, off),
                       M = __builtin_amdgcn_ds_bpermute(sq4, ml), S = __builtin_amdgcn_ds_bpermute(sq4, lstart);
-        const int32_t EL = ext_len(L);
+        const int32_t EL = ext_len<BIG>(L);
         const bool longlit = L >= kLongLit;
         int32_t r = t - pb;                 // index within the sequence's byte-parallel part
         if (longlit && r > EL) r += L;      // skip the wave-copied literals
@@ -174,9 +188,10 @@ __device__ __forceinline__ int32_t emit_seqs(const uint8_t* s, uint8_t* d, int32
             const int32_t ln = L < 15 ? L : 15;
             const int32_t mn = M ? (M - 4 < 15 ? M - 4 : 15) : 0;
             const uint32_t tokb = (uint32_t)((ln << 4) | mn);
-            const uint32_t lext = r < EL ? 255u : (uint32_t)(L - 15) % 255u;
-            const int32_t EM = ext_len(M - 4);
-            const uint32_t mext = r - (EL + L + 3) < EM - 1 ? 255u : (uint32_t)(M - 4 - 15) % 255u;
+            // the last length byte: what the 255s before it leave (no modulo)
+            const uint32_t lext = r < EL ? 255u : (uint32_t)(L - 15 - 255 * (EL - 1));
+            const int32_t EM = ext_len<BIG>(M - 4);
+            const uint32_t mext = r - (EL + L + 3) < EM - 1 ? 255u : (uint32_t)(M - 4 - 15 - 255 * (EM - 1));
             const bool win0 = (uint32_t)rel < 64u, win1 = (uint32_t)(rel + 64) < 64u;
             uint32_t litb = (win0 ? w0 : w1) & 0xFFu;
             if (r > EL && r <= EL + L && !win0 && !win1) litb = s[q];
@@ -194,7 +209,7 @@ __device__ __forceinline__ int32_t emit_seqs(const uint8_t* s, uint8_t* d, int32
         const int k = __builtin_ctzll(lm);
         const int32_t L = rdl(lit, k);
         const int32_t S = rdl(lstart, k);
-        uint8_t* o = d + op + rdl(obase, k) + 1 + ext_len(L);
+        uint8_t* o = d + op + rdl(obase, k) + 1 + ext_len<BIG>(L);
         for (int32_t x = 16 * (int32_t)lane; x < L; x += 16 * 64) {
             if (x + 16 <= L) {
                 st16(o + x, ld16(s + S + x));
@@ -373,7 +388,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BIG || HB > 
                 c -= bk;
                 len += bk;
                 const int32_t lit = st - anc;
-                const int32_t sz = isch ? seq_size(lit, len) : 0;
+                const int32_t sz = isch ? seq_size<BIG>(lit, len) : 0;
                 const int32_t psz = isch ? (lit >= kLongLit ? sz - lit : sz) : 0;
                 const int32_t isz = wave_incl_sum(sz), ipsz = wave_incl_sum(psz);
                 acc = rdl(isz, 63);
@@ -391,7 +406,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BIG || HB > 
             uint64_t maskB = 0;
             if (has_next) maskB = chunk_finish(B, p0 + 64, matchlimit, LB, backB, lane);
             if (ns > 0) {
-                const int32_t w = emit_seqs(s, d, op, cap, ns, q_ls, q_lit, q_off, q_ml, q_ob, q_pb, acc, pacc, p0,
+                const int32_t w = emit_seqs<BIG>(s, d, op, cap, ns, q_ls, q_lit, q_off, q_ml, q_ob, q_pb, acc, pacc, p0,
                                             A.v, vprev, lane);
                 if (w < 0) {
                     fail = true;
@@ -410,8 +425,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BIG || HB > 
         }
         if (!fail) {   // last literals (lz4.c:1266-1293)
             const int32_t lit = N - anchor;
-            const int32_t sz = seq_size(lit, 0);
-            const int32_t w = emit_seqs(s, d, op, cap, 1, anchor, lit, 0, 0, 0, 0, sz,
+            const int32_t sz = seq_size<BIG>(lit, 0);
+            const int32_t w = emit_seqs<BIG>(s, d, op, cap, 1, anchor, lit, 0, 0, 0, 0, sz,
                                         lit >= kLongLit ? sz - lit : sz, 1 << 30, 0u, 0u, lane);
             if (w < 0) {
                 fail = true;
