@@ -194,14 +194,14 @@ __device__ __forceinline__ int32_t emit_seqs(const uint8_t* s, uint8_t* d, int32
             const uint32_t mext = r - (EL + L + 3) < EM - 1 ? 255u : (uint32_t)(M - 4 - 15 - 255 * (EM - 1));
             const bool win0 = (uint32_t)rel < 64u, win1 = (uint32_t)(rel + 64) < 64u;
             uint32_t litb = (win0 ? w0 : w1) & 0xFFu;
-            if (r > EL && r <= EL + L && !win0 && !win1) litb = s[q];
+            if (r > EL && r <= EL + L && !win0 && !win1) litb = s[(uint32_t)q];
             const uint32_t byte = r == 0 ? tokb
                                   : r <= EL ? lext
                                   : r <= EL + L ? litb
                                   : r == EL + L + 1 ? (uint32_t)(O & 0xFF)
                                   : r == EL + L + 2 ? (uint32_t)((O >> 8) & 0xFF)
                                   : mext;
-            d[op + ob + r] = (uint8_t)byte;
+            d[(uint32_t)(op + ob + r)] = (uint8_t)byte;
         }
     }
     // long literals: coalesced 16-byte-per-lane copies
@@ -223,7 +223,7 @@ __device__ __forceinline__ int32_t emit_seqs(const uint8_t* s, uint8_t* d, int32
 
 // Bytes [p, p + 4) as a little-endian word, zero past n.
 __device__ __forceinline__ uint32_t load_word(const uint8_t* s, int32_t p, int32_t n) {
-    if (p + 4 <= n) return ld32(s + p);
+    if (p + 4 <= n) return ld32(s + (uint32_t)p);
     uint32_t x = 0;
     for (int k = 0; k < 3; ++k)
         if (p + k < n) x |= (uint32_t)s[p + k] << (8 * k);
@@ -273,12 +273,19 @@ __device__ __forceinline__ void chunk_issue(Chunk& C, const uint8_t* s, uint32_t
     // every address stays inside the block (N >= 4 here; p <= mlast when okc)
     const int32_t cs = C.okc ? cand : 0;
     const int32_t ps = C.okc ? p : 0;
-    C.xc = ld32(s + cs);
-    C.fa = ld16_guarded(s + ps + 4, N - ps - 4);
-    C.fc = ld16_guarded(s + cs + 4, N - cs - 4);
+    // (unsigned 32-bit offsets: the loads take the block base from SGPRs
+    // and skip the per-lane 64-bit address arithmetic)
+    C.xc = ld32(s + (uint32_t)cs);
+    if (p0 + 84 <= N) {   // every lane's 16 bytes in the block (cand < p): no guard
+        C.fa = ld16(s + (uint32_t)(ps + 4));
+        C.fc = ld16(s + (uint32_t)(cs + 4));
+    } else {
+        C.fa = ld16_guarded(s + ps + 4, N - ps - 4);
+        C.fc = ld16_guarded(s + cs + 4, N - cs - 4);
+    }
     const bool bk = C.okc && cand >= 4;
-    C.bp = bk ? ld32(s + p - 4) : 0u;
-    C.bc = bk ? ld32(s + cand - 4) : 1u;
+    C.bp = bk ? ld32(s + (uint32_t)(p - 4)) : 0u;
+    C.bc = bk ? ld32(s + (uint32_t)(cand - 4)) : 1u;
 }
 
 __device__ __forceinline__ uint64_t chunk_finish(const Chunk& C, int32_t p0, int32_t matchlimit, int32_t& L,
