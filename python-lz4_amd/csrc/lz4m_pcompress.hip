@@ -49,14 +49,24 @@ constexpr uint32_t kEmpty = 0xFFFFu;
 template <int HB>
 __device__ __forceinline__ uint32_t phash(uint32_t v) { return (v * 2654435761u) >> (32 - HB); }
 
-// equal leading bytes of two 16-byte windows (0..16)
+// equal leading bytes of two 16-byte windows (0..16), branch-free: v_ffbl
+// gives ~0u for a zero word, so OR-ing the word's bit base (32 / 64 / 96)
+// keeps "no difference" the largest value and one unsigned min over the four
+// words finds the first differing bit (the divergent if-chain ran every
+// level for the lanes without a candidate, which compare equal windows)
+__device__ __forceinline__ uint32_t ffbl(uint32_t x) {
+    uint32_t r;
+    asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(x));   // ~0u for x == 0 (the compiler re-tests zero otherwise)
+    return r;
+}
+
 __device__ __forceinline__ uint32_t eq_prefix16(u32x4 a, u32x4 b) {
-    const uint32_t x0 = a.x ^ b.x, x1 = a.y ^ b.y, x2 = a.z ^ b.z, x3 = a.w ^ b.w;
-    if (x0) return __builtin_ctz(x0) >> 3;
-    if (x1) return 4 + (__builtin_ctz(x1) >> 3);
-    if (x2) return 8 + (__builtin_ctz(x2) >> 3);
-    if (x3) return 12 + (__builtin_ctz(x3) >> 3);
-    return 16;
+    const uint32_t f0 = ffbl(a.x ^ b.x);
+    const uint32_t f1 = ffbl(a.y ^ b.y) | 32u;
+    const uint32_t f2 = ffbl(a.z ^ b.z) | 64u;
+    const uint32_t f3 = ffbl(a.w ^ b.w) | 96u;
+    const uint32_t m = __builtin_elementwise_min(__builtin_elementwise_min(f0, f1), __builtin_elementwise_min(f2, f3));
+    return m >= 128u ? 16u : m >> 3;
 }
 
 __device__ __forceinline__ int32_t rdl(int32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
