@@ -407,7 +407,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BIG || HB > 
                 const int32_t lit = st - anc;
                 const int32_t sz = isch ? seq_size<BIG>(lit, len) : 0;
                 const int32_t psz = isch ? (lit >= kLongLit ? sz - lit : sz) : 0;
-                const int32_t isz = wave_incl_sum(sz), ipsz = wave_incl_sum(psz);
+                int32_t isz, ipsz;
+                if (BIG) {
+                    isz = wave_incl_sum(sz);
+                    ipsz = wave_incl_sum(psz);
+                } else {
+                    // one scan for both: a step's byte-parallel total stays
+                    // far below 2^14 (short literals, tokens, offsets, length
+                    // bytes of <= 64 KiB matches) and its output below 2^18
+                    const int32_t both = wave_incl_sum((sz << 14) | psz);
+                    isz = (int32_t)((uint32_t)both >> 14);
+                    ipsz = both & 0x3FFF;
+                }
                 acc = rdl(isz, 63);
                 pacc = rdl(ipsz, 63);
                 const int addr = (isch ? count_below(chosen) : 63) << 2;
