@@ -1654,7 +1654,7 @@ int env_int(const char* name, int dflt) {
     return v > 0 ? v : dflt;
 }
 
-enum Decoder { kAuto = 0, kLaneDec, kCoopDec, kHistDec, kRowsDec, kDirectDec };
+enum Decoder { kAuto = 0, kLaneDec, kCoopDec, kHistDec, kRowsDec, kDirectDec, kQuadDec };
 
 // LZ4M_DECODER forces a decoder (A/B measurements, tests): lane | hist | coop |
 // rows | direct; unset = by batch size and scratch.
@@ -1667,6 +1667,7 @@ int decoder_env() {
         if (strcmp(e, "hist") == 0) return (int)kHistDec;
         if (strcmp(e, "rows") == 0) return (int)kRowsDec;
         if (strcmp(e, "direct") == 0) return (int)kDirectDec;
+        if (strcmp(e, "quad") == 0) return (int)kQuadDec;
         return (int)kAuto;
     }();
     return mode;
@@ -1686,7 +1687,7 @@ extern "C" int lz4m_decompress_batch_sel(const uint8_t* d_src, const int64_t* d_
                                          uint8_t* d_dst, const int64_t* d_dst_off, const int32_t* d_dst_cap,
                                          int32_t* d_status, int64_t n, void* d_work, size_t work_bytes, int decoder,
                                          lz4m_stream_t stream) {
-    if (n < 0 || decoder < 0 || decoder > kDirectDec) return LZ4M_EINVAL;
+    if (n < 0 || decoder < 0 || decoder > kQuadDec) return LZ4M_EINVAL;
     if (n == 0) return 0;
     hipStream_t st = (hipStream_t)stream;
     if (decoder == kAuto) decoder = decoder_env();
@@ -1710,14 +1711,15 @@ extern "C" int lz4m_decompress_batch_sel(const uint8_t* d_src, const int64_t* d_
         else if (n <= coop_max) decoder = kHistDec;
         else decoder = kLaneDec;
     }
-    if (decoder == kRowsDec && !rows_fit) decoder = n <= coop_max ? kHistDec : kLaneDec;
-    if (decoder == kRowsDec) {
+    if ((decoder == kRowsDec || decoder == kQuadDec) && !rows_fit) decoder = n <= coop_max ? kHistDec : kLaneDec;
+    if (decoder == kRowsDec || decoder == kQuadDec) {
+        const int quad = decoder == kQuadDec;
         int pg = 1, eg = 1;
-        lz4m_rows_grids(n, &pg, &eg);
+        lz4m_rows_grids(n, quad, &pg, &eg);
         const int rc = lz4m_rows_launch(d_src, d_src_off, d_src_len, d_dst, d_dst_off, d_dst_cap, n, d_work, work_bytes,
-                                        pg, eg, st);
+                                        pg, eg, quad, st);
         if (rc != 0) return rc;
-        const RowMeta* meta = reinterpret_cast<const RowMeta*>(static_cast<const uint8_t*>(d_work) + 64);
+        const RowMeta* meta = reinterpret_cast<const RowMeta*>(static_cast<const uint8_t*>(d_work) + kRowsMeta);
         const int64_t grid = (n + 255) / 256;
         hipLaunchKernelGGL((decompress_kernel<false, true>), dim3((uint32_t)grid), dim3(256), 0, st, d_src, d_src_off,
                            d_src_len, d_dst, d_dst_off, d_dst_cap, nullptr, nullptr, nullptr, d_status, n, meta);
