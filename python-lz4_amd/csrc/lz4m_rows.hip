@@ -145,6 +145,23 @@ __device__ __forceinline__ void lds_put_bf(lds_u8* p, lds_u8* dummy, u32x4 v, in
     *(b1 ? p + (km & 14) : dummy) = (uint8_t)(b2 ? (d2 >> 16) : d2);
 }
 
+// Exactly k (1..) bytes (k >= 16: 16) of v at LDS address p: each piece
+// written by the lanes that need it only (an LDS access costs per active
+// lane), with no branches around the pieces.
+__device__ __forceinline__ void lds_put_masked(lds_u8* p, u32x4 v, int32_t k) {
+    const bool full = k >= 16;
+    const uint32_t km = full ? 0u : (uint32_t)k;
+    if (full) lds_st16(p, v);
+    const uint64_t lo = ((uint64_t)v.y << 32) | v.x;
+    if (km & 8) __builtin_memcpy((uint8_t*)p, &lo, 8);
+    const uint32_t d4 = (km & 8) ? v.z : v.x;
+    if (km & 4) __builtin_memcpy((uint8_t*)(p + (km & 8)), &d4, 4);
+    const uint32_t d2 = (km & 4) ? ((km & 8) ? v.w : v.y) : d4;
+    const uint16_t h2 = (uint16_t)d2;
+    if (km & 2) __builtin_memcpy((uint8_t*)(p + (km & 12)), &h2, 2);
+    if (km & 1) *(p + (km & 14)) = (uint8_t)((km & 2) ? (d2 >> 16) : d2);
+}
+
 // Exactly k bytes (k >= 16: 16) of v at global address p.
 __device__ __forceinline__ void gbl_put(uint8_t* p, u32x4 v, int32_t k) {
     if (k >= 16) {
@@ -440,6 +457,9 @@ __global__ __launch_bounds__(kPWG) void rows_parse_kernel(const uint8_t* __restr
 #define LZ4M_ROWS_H 2048
 #endif
 constexpr int32_t kRowsH = LZ4M_ROWS_H;
+#ifndef LZ4M_ROWS_LITPUT
+#define LZ4M_ROWS_LITPUT 0   // A/B: 1 = literal put only for lanes with a literal, 2 = and per piece
+#endif
 #ifndef LZ4M_ROWS_PUTMASK
 #define LZ4M_ROWS_PUTMASK 3   // 0 = branch-free dummy-slot puts (round 2); 1 = pass puts exec-masked; 2 = literal puts too; 3 = the whole pass body masked to the ready lanes
 #endif
@@ -750,8 +770,10 @@ __global__ __launch_bounds__(64) void rows_exec_kernel(const uint8_t* __restrict
         const int32_t lit = P.lit, off = P.off, ml = P.ml, o = P.o;
         const int32_t m = o + lit, mend = m + ml, s0 = m - off;
         // literals: bytes lp.. of the input (exact, branch-free); longer ones rare
-#if LZ4M_ROWS_PUTMASK >= 2
-        if (u) lds_put(HB + (o - base), P.x0, lit);
+#if LZ4M_ROWS_LITPUT == 1
+        if (u && lit > 0) lds_put_bf(HB + (o - base), DUM, P.x0, lit);
+#elif LZ4M_ROWS_LITPUT == 2
+        if (u && lit > 0) lds_put_masked(HB + (o - base), P.x0, lit);
 #else
         lds_put_bf(HB + (o - base), DUM, P.x0, u ? lit : 0);
 #endif
