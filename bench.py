@@ -171,14 +171,17 @@ def cpu_baseline(host_blocks: np.ndarray, comp_host: list, seconds: float = 10.0
     return res
 
 
-def config5(src, n, world, rank, dev, wave_blocks, waves, total_blocks):
-    """BASELINE config 5: a shard larger than HBM is
-    compressed in waves over a resident working set (here: the rank's 1 M
-    generated blocks, a different window of them each wave), each wave
-    compacted and gathered at rank 0 over RCCL (lz4._dist), the gather of
-    wave k overlapped with the compression of wave k+1.  Weak scaling:
-    `waves` waves per rank; strong scaling: `total_blocks` over all ranks.
-    Parallel-parse compressor (config 3's kernel)."""
+def config5(src, n, world, rank, dev, wave_blocks, waves, strong_total):
+    """BASELINE config 5: 256 M x 64 KiB = 16 TiB cannot be
+    device-resident, so every rank compresses its share in waves of
+    `wave_blocks` over a resident working set (the rank's generated blocks,
+    a different window of them each wave when the wave is smaller), each
+    wave compacted and gathered at rank 0 over RCCL (lz4._dist), which
+    consumes every page (XXH32 of every block, LZ4F's block checksum) -- the
+    gather of wave k runs beside the compression of wave k+1.  Weak scaling:
+    `waves` waves per rank (32 x 1 M at 8 ranks = the stated 256 M job);
+    strong scaling: `strong_total` blocks over all ranks.  Parallel-parse
+    compressor (config 3's kernel)."""
     from lz4._dist import compress_gather_waves
     bw = min(wave_blocks, n)
     cap = N.compress_bound(BLOCK)
@@ -188,53 +191,69 @@ def config5(src, n, world, rank, dev, wave_blocks, waves, total_blocks):
     slots = torch.empty(bw * cap16, dtype=torch.uint8, device=dev)
     slot_off = torch.arange(bw, dtype=torch.int64, device=dev) * cap16
     slot_cap = torch.full((bw,), cap, dtype=torch.int32, device=dev)
-    out_len = torch.empty(bw, dtype=torch.int32, device=dev)
-    comp = [torch.empty(bw * cap16, dtype=torch.uint8, device=dev) for _ in range(2)]
+    lens = [torch.empty(bw, dtype=torch.int32, device=dev) for _ in range(2)]
+    # compacted waves: sized for a ratio >= 1.5 (silesia-like is ~1.9); a wave
+    # that does not fit fails the run below instead of overflowing
+    comp_cap = bw * BLOCK * 2 // 3
+    comp = [torch.empty(comp_cap, dtype=torch.uint8, device=dev) for _ in range(2)]
     windows = max(1, n // bw)
+    digest = torch.zeros(1, dtype=torch.int64, device=dev)
+    overflow = torch.zeros(1, dtype=torch.int64, device=dev)
+    sums = torch.empty(8192, dtype=torch.int32, device=dev)
+    page_blocks = 4096
 
     def compress_wave(w):
         so = base_off + ((w % windows) * bw) * BLOCK
-        N.launch_compress(src, so, src_len, slots, slot_off, slot_cap, out_len, bw, N.PARSE_PARALLEL, 1)
-        offs = N.exclusive_scan(out_len)
-        buf = comp[w & 1]
-        N.gather(slots, slot_off, out_len, buf, offs, bw)
-        total = int(offs[bw])   # the wave's compacted size (host needs it to post the transfers)
-        return buf[:total], out_len
+        ln = lens[w & 1]
+        N.launch_compress(src, so, src_len, slots, slot_off, slot_cap, ln, bw, N.PARSE_PARALLEL, 1)
+        offs = N.exclusive_scan(ln)
+        # capacity check on the device: a too-large wave is compacted to zero
+        # blocks (its lengths zeroed) and counted, never written past comp
+        over = offs[bw] > comp_cap
+        ln.masked_fill_(over, 0)
+        offs.masked_fill_(over, 0)
+        overflow.add_(over)
+        N.gather(slots, slot_off, ln, comp[w & 1], offs, bw)
+        return comp[w & 1], ln
+
+    def consume(w, r, first, buf, blens):
+        k = blens.numel()
+        offs = N.exclusive_scan(blens)
+        N.launch_xxh32_batch(buf, offs, blens.to(torch.int64), 0, sums, k)
+        digest.add_(sums[:k].to(torch.int64).sum())
 
     def run(nw):
         box = {}
-        if world == 1:   # no exchange: compress + compact only
-            def go():
-                cb = 0
-                for w in range(nw):
-                    c, _ = compress_wave(w)
-                    cb += c.numel()
-                box["st"] = {"comp_bytes": cb, "gathered_bytes": 0}
-        else:
-            def go():
-                box["st"] = compress_gather_waves(compress_wave, nw, root=0)
-        wall, _ = time_kernel(go, 1, 1, world)
+
+        def go():
+            box["st"] = compress_gather_waves(compress_wave, nw, root=0, consume=consume, page_blocks=page_blocks)
+
+        wall, _ = time_kernel(go, 1, 0, world)
         st = box["st"]
-        res = {"waves_per_rank": nw, "blocks_per_rank": nw * bw, "seconds": round(wall, 4),
-               "aggregate_gib_s": round(world * nw * bw * BLOCK / wall / GIB, 2),
-               "ratio": round(nw * bw * BLOCK / max(st["comp_bytes"], 1), 4)}
+        if int(overflow.item()):
+            raise SystemExit("config 5: a wave did not fit its compaction buffer")
+        res = {"waves_per_rank": nw, "blocks_per_rank": nw * bw, "total_blocks": world * nw * bw,
+               "seconds": round(wall, 3), "aggregate_gib_s": round(world * nw * bw * BLOCK / wall / GIB, 2),
+               "ratio": round(nw * bw * BLOCK / max(st["comp_bytes"], 1), 4),
+               "host_waits_per_wave": st["host_waits"] // max(1, nw)}
+        g = torch.tensor([st["gathered_bytes"]], dtype=torch.int64, device=dev)
         if world > 1:
-            g = torch.tensor([st["gathered_bytes"]], dtype=torch.int64, device=dev)
             torch.distributed.all_reduce(g)
-            res["root_ingress_gb_s"] = round(int(g) / wall / 1e9, 2)
+        res["root_consumed_gb_s"] = round(int(g) / wall / 1e9, 2)
+        res["pages_at_root"] = st["pages"] if rank == 0 else None
         return res
 
+    # warm the path (allocations, RCCL peer connections) with one wave
+    run(1)
     out = {"wave_blocks_per_rank": bw, "block_size": BLOCK, "parse": "parallel (LZ4M_PARSE_PARALLEL)",
-           "gather": "rank 0 over RCCL, overlapped with the next wave" if world > 1 else "none (1 rank)",
+           "gather": ("rank 0 over RCCL (isend/irecv pages of %d blocks), overlapped with the next wave"
+                      % page_blocks) if world > 1 else "none (1 rank); rank 0 consumes its own pages",
+           "root_consumer": "XXH32 of every gathered block (lz4m_xxh32_batch), one page at a time",
            "weak": run(waves)}
-    out["strong"] = dict(run(max(1, total_blocks // (world * bw))), total_blocks=total_blocks)
-    # the same waves without the exchange, for the compress-only rate per rank
-    if world > 1:
-        t0 = time.perf_counter()
-        for w in range(waves):
-            compress_wave(w)
-        torch.cuda.synchronize()
-        out["compress_only_gib_s_per_rank"] = round(waves * bw * BLOCK / (time.perf_counter() - t0) / GIB, 2)
+    sw = max(1, strong_total // (world * bw))
+    out["strong"] = dict(out["weak"], same_run_as_weak=True) if sw == waves else run(sw)
+    out["strong"]["total_blocks_fixed"] = strong_total
+    out["stated_config_fraction"] = round(world * waves * bw / float(1 << 28), 4)
     del slots, comp
     return out
 
@@ -317,11 +336,12 @@ def main():
                     help="config 4: GiB of input in one LZ4 frame of 4 MiB independent blocks + content checksum; 0 = skip")
     ap.add_argument("--e2e-blocks", type=int, default=1 << 18,
                     help="blocks of the host-to-host (PCIe-inclusive) extra line; 0 = skip")
-    ap.add_argument("--c5-wave-blocks", type=int, default=1 << 16,
+    ap.add_argument("--c5-wave-blocks", type=int, default=1 << 20,
                     help="config 5: 64 KiB blocks per rank per wave (compressed, compacted, gathered at rank 0)")
-    ap.add_argument("--c5-waves", type=int, default=4, help="config 5 weak scaling: waves per rank")
-    ap.add_argument("--c5-total", type=int, default=1 << 19,
-                    help="config 5 strong scaling: blocks in total over all ranks; 0 = skip config 5")
+    ap.add_argument("--c5-waves", type=int, default=32,
+                    help="config 5 weak scaling: waves per rank (32 x 1 M at 8 GPUs = the stated 256 M blocks)")
+    ap.add_argument("--c5-total", type=int, default=1 << 25,
+                    help="config 5 strong scaling: blocks in total over all ranks (32 M); 0 = skip config 5")
     ap.add_argument("--c1-blocks", type=int, default=1000,
                     help="config 1: random 64 KiB blocks through the per-call lz4.block API; 0 = skip")
     args = ap.parse_args()
@@ -345,7 +365,11 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        torch.distributed.init_process_group("nccl", device_id=dev)
+        # RCCL on high-priority streams: config 5's gather shares the GPU with
+        # compression kernels
+        opts = torch.distributed.ProcessGroupNCCL.Options()
+        opts.is_high_priority_stream = True
+        torch.distributed.init_process_group("nccl", device_id=dev, pg_options=opts)
     N.lib()
 
     n = args.blocks
@@ -406,7 +430,7 @@ def main():
     c_off = offs[:n].clone()
     c_len = out_len.clone()
     comp_sample = None
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and not args.no_cpu:   # cpu_baseline at every N (rank 0, after the timed regions)
         k = min(n, 16384)
         comp_host_np = comp[: int(offs[k])].cpu().numpy()
         oh = offs[: k + 1].cpu().numpy()
@@ -440,11 +464,6 @@ def main():
     extra["decompress_mid_batch"] = {"blocks": nm, "gib_s": round(world * nm * BLOCK / (m_wall / args.steps) / GIB, 2),
                                      "kernel_ms": round(m_ev * 1e3, 3),
                                      "kernel": "default dispatch: row decoder (>= 32 768 blocks)"}
-
-    # ---- config 5: compress in waves, gather every wave at rank 0 (RCCL) ----
-    if args.c5_total > 0:
-        extra["config5"] = config5(src, n, world, rank, dev, args.c5_wave_blocks, args.c5_waves, args.c5_total)
-        log("[bench] config 5 done")
 
     # ---- extra: end to end from pinned host memory (PCIe-inclusive) ----
     # lz4.block.decompress_host: chunks of 65 536 blocks pipelined over three
@@ -507,6 +526,16 @@ def main():
     torch.cuda.empty_cache()
 
     log("[bench] decode done")
+    # ---- config 5: compress in waves, gather every wave at rank 0 (RCCL) ----
+    # (after config 2's buffers are gone: a 1 M-block wave needs its bound-sized
+    # slots and two compaction buffers beside the 64 GiB working set)
+    del comp
+    dst = None
+    torch.cuda.empty_cache()
+    if args.c5_total > 0:
+        extra["config5"] = config5(src, n, world, rank, dev, args.c5_wave_blocks, args.c5_waves, args.c5_total)
+        torch.cuda.empty_cache()
+        log("[bench] config 5 done")
     # ---- extra: config 4, one frame of 4 MiB independent blocks + XXH32 content checksum ----
     if args.frame_gib > 0:
         from lz4.frame._frame import _compress_frame

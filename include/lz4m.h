@@ -122,19 +122,16 @@ const char* lz4m_version_string(void);
  *             finisher for each block's tail (needs the scratch of
  *             lz4m_decompress_workspace_size);
  *   hist   -- one wavefront per block with its recent output in LDS (small and
- *             mid-size batches, large blocks);
- *   lane   -- one lane per block, LDS-staged (large batches, 64 bytes of scratch);
- *   coop, direct -- earlier designs, kept for A/B measurements.
- * This entry point takes 64 bytes of stream-ordered scratch per call
- * (hipMallocAsync / hipFreeAsync on `stream`), so it never uses the rows
- * decoder; pass scratch through lz4m_decompress_batch_ws for that.
+ *             mid-size batches, large blocks, and any batch without scratch);
+ *   quad   -- an experimental 4-lane-per-block executor (A/B measurements only).
+ * This entry point takes no scratch, so it always uses the hist decoder; pass
+ * scratch through lz4m_decompress_batch_ws for the rows decoder.
  */
 int lz4m_decompress_batch(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len,
                           uint8_t* d_dst, const int64_t* d_dst_off, const int32_t* d_dst_cap,
                           int32_t* d_status, int64_t n, lz4m_stream_t stream);
 
-/* Minimum device scratch of lz4m_decompress_batch_ws (the work-queue counter
- * of the lane decoder). */
+/* Minimum device scratch of lz4m_decompress_batch_ws (64 bytes). */
 size_t lz4m_decompress_workspace_bytes(void);
 
 /* Device scratch for the fastest decode of n blocks whose compressed sizes
@@ -147,21 +144,20 @@ size_t lz4m_decompress_workspace_size(int64_t n, int64_t src_bytes);
 
 /* lz4m_decompress_batch with caller-provided device scratch (8-byte aligned,
  * at least lz4m_decompress_workspace_bytes(), not shared with a concurrently
- * running call).  Picks the decoder by batch size and scratch (env
- * LZ4M_DECODER=rows|hist|lane|coop|direct forces one; LZ4M_ROWS_MIN_BLOCKS and
- * LZ4M_COOP_MAX_BLOCKS move the switch-overs). */
+ * running call).  Picks the decoder by batch size and scratch: rows from
+ * LZ4M_ROWS_MIN_BLOCKS (32 768) blocks when the scratch fits, else hist
+ * (env LZ4M_DECODER=rows|hist|quad forces one). */
 int lz4m_decompress_batch_ws(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len,
                              uint8_t* d_dst, const int64_t* d_dst_off, const int32_t* d_dst_cap,
                              int32_t* d_status, int64_t n, void* d_work, size_t work_bytes,
                              lz4m_stream_t stream);
 
-/* lz4m_decompress_batch_ws with an explicit decoder (tests, A/B runs). */
+/* lz4m_decompress_batch_ws with an explicit decoder (tests, A/B runs); any
+ * other id (1, 2 and 5 were retired decoders) returns LZ4M_EINVAL. */
 #define LZ4M_DECODER_AUTO   0
-#define LZ4M_DECODER_LANE   1
-#define LZ4M_DECODER_COOP   2
 #define LZ4M_DECODER_HIST   3
 #define LZ4M_DECODER_ROWS   4
-#define LZ4M_DECODER_DIRECT 5
+#define LZ4M_DECODER_QUAD   6
 int lz4m_decompress_batch_sel(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len,
                               uint8_t* d_dst, const int64_t* d_dst_off, const int32_t* d_dst_cap,
                               int32_t* d_status, int64_t n, void* d_work, size_t work_bytes, int decoder,

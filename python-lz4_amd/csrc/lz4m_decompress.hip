@@ -54,66 +54,7 @@ struct Lane {
     int64_t ip, op;
     int32_t result;
     bool fast, live;
-    // STAGE mode (the hot kernel): an LDS output stage holding output bytes
-    // [F - 16, op) at offset p - F + 16 ([0, F) is in HBM, F % 64 == 0) and
-    // an LDS input window holding compressed bytes [ib, ib + 64).
-    lds_u8* stage;
-    int64_t F;
-    lds_u8* win;
-    int64_t ib;
 };
-
-// ------------------------------------------------------ LDS staging (hot kernel)
-// Output is assembled in a per-lane 96-byte LDS stage and leaves for HBM in whole,
-// contiguous 64-byte chunks (4 x 16-byte stores by one lane): every HBM line
-// is written once, instead of piecemeal by 1-16 byte stores from thousands of
-// interleaved lane streams.  The token stream is read through a per-lane
-// 64-byte window refilled by 16-byte loads of consecutive addresses, so each
-// compressed byte crosses the memory hierarchy about once (reading tokens
-// straight from HBM cost ~3 cache-line fetches per sequence).  Both buffers
-// are linear and rebased as they advance, so every access is one unaligned
-// ds_read/ds_write_b128 without wrap-around logic; stores into the stage are
-// wild 16-byte stores (like the reference's wild copies) and only the final
-// partial chunk is written to HBM byte-exactly.
-// The stage holds output [F - 16, F + 80): stores at p < F + 64 (16 bytes,
-// wild) stay inside, and [F - 16, F) keeps the bytes a short match may
-// still read.  96 + 64 bytes per lane is 40 KB per 256-lane workgroup, so 4
-// workgroups (16 waves) fit a CU's 160 KB of LDS -- the decoder is latency
-// bound, and 16 waves/CU decode 1.15-1.3x faster than 12 with 128-byte
-// stages (tools/prof_decode.py, MI355X).
-constexpr int kStage = 96;
-constexpr int kWin = 64;
-
-__device__ __forceinline__ lds_u8* stage_at(const Lane& L, int64_t p) { return L.stage + (p - L.F + 16); }
-
-// Chunk [F, F + 64) is final: write it to HBM and rebase the stage by 64
-// (the 32 bytes [F + 48, F + 80) move to the front).
-__device__ __forceinline__ void stage_flush(Lane& L) {
-    const u32x4 a = lds_ld16(L.stage + 16), b = lds_ld16(L.stage + 32), c = lds_ld16(L.stage + 48),
-                d = lds_ld16(L.stage + 64);
-    const u32x4 e = lds_ld16(L.stage + 80);
-    uint8_t* o = L.dst + L.F;
-    st16(o, a);
-    st16(o + 16, b);
-    st16(o + 32, c);
-    st16(o + 48, d);
-    lds_st16(L.stage, d);
-    lds_st16(L.stage + 16, e);
-    L.F += 64;
-}
-
-// Before a 16-byte store at output position p (all bytes below p final):
-// keep p < F + 64, so stores stay inside the stage.
-__device__ __forceinline__ void stage_sync(Lane& L, int64_t p) {
-    if (p >= L.F + 64) stage_flush(L);
-}
-
-// 16 output bytes from q, a match source: the stage if q >= F - 16, else
-// HBM (then q + 16 <= F: already flushed).
-__device__ __forceinline__ u32x4 out_read16(const Lane& L, int64_t q) {
-    if (q >= L.F - 16) return lds_ld16(stage_at(L, q));
-    return ld16(L.dst + q);
-}
 
 // Store exactly k (0..16) bytes of v at p (any alignment).
 __device__ __forceinline__ void put_exact(uint8_t* p, u32x4 v, uint32_t k) {
@@ -142,112 +83,13 @@ __device__ __forceinline__ void put_exact(uint8_t* p, u32x4 v, uint32_t k) {
 
 // ------------------------------------------------ input reads (general path)
 // The general state machine reads the compressed block byte by byte (length
-// bytes, offsets) and in 16-byte pieces (token window, literals).  In STAGE
-// mode these come from the lane's LDS input window [ib, ib + 64) when they
-// lie inside it (it holds the block's bytes, zeros past iend -- the same
-// values ld16_guarded returns), else from HBM: a general step then costs LDS
-// latencies instead of a chain of dependent HBM round trips.
-template <bool STAGE>
-__device__ __forceinline__ uint32_t in_byte(const Lane& L, int64_t p) {
-    if (STAGE) {
-        const int64_t d = p - L.ib;
-        if (d >= 0 && d < kWin) return L.win[d];
-    }
-    return L.src[p];
-}
+// bytes, offsets) and in 16-byte pieces (token window, literals).
+__device__ __forceinline__ uint32_t in_byte(const Lane& L, int64_t p) { return L.src[p]; }
 
-template <bool STAGE>
-__device__ __forceinline__ u32x4 in16(const Lane& L, int64_t p) {
-    if (STAGE) {
-        const int64_t d = p - L.ib;
-        if (d >= 0 && d <= kWin - 16) return lds_ld16(L.win + d);
-    }
-    return ld16_guarded(L.src + p, L.iend - p);
-}
+__device__ __forceinline__ u32x4 in16(const Lane& L, int64_t p) { return ld16_guarded(L.src + p, L.iend - p); }
 
-template <bool STAGE>
 __device__ __forceinline__ uint32_t in_le16(const Lane& L, int64_t p) {
-    return in_byte<STAGE>(L, p) | (in_byte<STAGE>(L, p + 1) << 8);
-}
-
-// Literal of len <= 64 bytes read from the compressed block.
-__device__ __forceinline__ void stage_literal(Lane& L, int64_t op, int64_t ip, int64_t len) {
-    for (int64_t i = 0; i < len; i += 16) {
-        stage_sync(L, op + i);
-        lds_st16(stage_at(L, op + i), in16<true>(L, ip + i));
-    }
-}
-
-// Match of len <= 64 bytes (zeros for off == 0, lz4.c:2300-2307).
-__device__ __forceinline__ void stage_match(Lane& L, int64_t op, int64_t off, int64_t len) {
-    if (off >= 16) {
-        for (int64_t i = 0; i < len; i += 16) {
-            stage_sync(L, op + i);
-            lds_st16(stage_at(L, op + i), out_read16(L, op + i - off));
-        }
-        return;
-    }
-    u32x4 pat;
-    int64_t step;
-    if (off == 0) {
-        pat = u32x4{0, 0, 0, 0};
-        step = 16;
-    } else {
-        stage_sync(L, op);
-        pat = period_pattern(out_read16(L, op - off), (uint32_t)off);   // op - off >= F - 16
-        step = 16 - (16 % off);
-    }
-    for (int64_t i = 0; i < len; i += step) {
-        stage_sync(L, op + i);
-        lds_st16(stage_at(L, op + i), pat);
-    }
-}
-
-// Block done (or failed): flush [F, end) byte-exactly.
-__device__ __forceinline__ void stage_finish(Lane& L, int64_t end) {
-    while (L.F + 64 <= end) stage_flush(L);
-    for (int64_t p = L.F; p < end; p += 16) {
-        put_exact(L.dst + p, lds_ld16(stage_at(L, p)), (uint32_t)(end - p < 16 ? end - p : 16));
-    }
-}
-
-// After a wave-cooperative copy wrote [.., E) straight to HBM: restart the
-// stage at F = E rounded down to 64, reloading [F - 16, E) from HBM.
-__device__ __forceinline__ void stage_reload(Lane& L, int64_t E) {
-    L.F = E & ~(int64_t)63;
-    for (int64_t x = L.F - 16; x < E; x += 16) {
-        if (x >= 0) lds_st16(stage_at(L, x), ld16_guarded(L.dst + x, L.oend - x));
-    }
-}
-
-// Input window: make it cover [ip, ip + 32) (ip - ib < 32).
-__device__ __forceinline__ void win_sync(Lane& L) {
-    const int64_t d = L.ip - L.ib;
-    if (d < 32) return;
-    const bool shift = d < 64;
-    const int64_t nb = shift ? L.ib + 32 : (L.ip & ~(int64_t)15);
-    const int64_t first = shift ? nb + 32 : nb;
-    u32x4 k0 = u32x4{0, 0, 0, 0}, k1 = k0;
-    if (shift) {
-        k0 = lds_ld16(L.win + 32);
-        k1 = lds_ld16(L.win + 48);
-    }
-    u32x4 v[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int64_t x = nb + 16 * k;
-        v[k] = u32x4{0, 0, 0, 0};
-        if (x >= first) v[k] = x + 16 <= L.iend ? ld16(L.src + x) : ld16_guarded(L.src + x, L.iend - x);
-    }
-    if (shift) {
-        lds_st16(L.win, k0);
-        lds_st16(L.win + 16, k1);
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        if (nb + 16 * k >= first) lds_st16(L.win + 16 * k, v[k]);
-    }
-    L.ib = nb;
+    return in_byte(L, p) | (in_byte(L, p + 1) << 8);
 }
 
 // ---------------------------------------------------------------- lane copies
@@ -304,7 +146,7 @@ __device__ __forceinline__ void lane_match(uint8_t* d, int64_t off, int64_t len,
 // Literal bytes never overlap their destination, so each lane requests four
 // 16-byte pieces before storing any: a long literal (a stored-looking block's
 // 64 KiB) waits on one memory round trip per 4 KiB instead of per 1 KiB.
-template <int kU = 4>   // pieces per lane per round trip (1 where registers are short: the stage kernel)
+template <int kU = 4>   // pieces per lane per round trip (1 where registers are short: the dictionary kernel)
 __device__ __forceinline__ void wave_literal(uint8_t* d, const uint8_t* s, int64_t len, int64_t d_room,
                                              int64_t s_room, uint32_t lane) {
     for (int64_t base = 0; base < len; base += 16 * kWave * kU) {
@@ -372,11 +214,10 @@ __device__ __forceinline__ void wave_match(uint8_t* d, int64_t off, int64_t len,
 // ------------------------------------------------------------ lane decode
 // read_variable_length (lz4.c:1903-1928).  On failure *ip is the position
 // the reference reports.
-template <bool STAGE>
 __device__ __forceinline__ bool read_len(const Lane& L, int64_t& ip, int64_t ilimit, bool initial_check,
                                          int64_t& out) {
     if (initial_check && ip >= ilimit) return false;
-    if (!STAGE) {
+    {
         // 16 bytes per load: a run of 255s (a long literal or match, e.g. the
         // 257 length bytes of a stored-looking 64 KiB block) costs one memory
         // round trip per 16 bytes instead of per byte.  Same outcome as the
@@ -413,51 +254,29 @@ __device__ __forceinline__ bool read_len(const Lane& L, int64_t& ip, int64_t ili
             ip += 16;
         }
     }
-    int64_t len = 0;
-    uint32_t s;
-    do {
-        s = in_byte<STAGE>(L, ip);
-        ++ip;
-        len += s;
-        if (ip > ilimit) return false;
-    } while (s == 255);
-    out = len;
-    return true;
 }
 
-template <bool STAGE>
 __device__ __forceinline__ void emit_literal(Lane& L, int64_t ip, int64_t op, int64_t lit, Copy& c,
                                              bool deferred) {
     if (lit == 0) return;
     if (deferred || lit > kCoopMin) {
         c = Copy{kLiteral, op, ip, lit};
-    } else if (STAGE) {
-        stage_literal(L, op, ip, lit);
     } else {
         lane_copy(L.dst + op, L.src + ip, lit, L.oend - op, L.iend - ip);
     }
 }
 
-template <bool STAGE>
 __device__ __forceinline__ void emit_match(Lane& L, int64_t op, int64_t off, int64_t ml, Copy& c, bool deferred) {
     if (deferred || ml > kCoopMin) {
         c = Copy{kMatch, op, off, ml};
-    } else if (STAGE) {
-        stage_match(L, op, off, ml);
     } else {
         lane_match(L.dst + op, off, ml, L.oend - op);
     }
 }
 
 // Literal bytes 1..lit (lit <= 14) of the token window.
-template <bool STAGE>
 __device__ __forceinline__ void window_literal(Lane& L, int64_t op, u32x4 w, int64_t lit) {
-    if (STAGE) {
-        stage_sync(L, op);
-        lds_st16(stage_at(L, op), window_shift1(w));   // wild 16-byte store
-    } else {
-        st16(L.dst + op, window_shift1(w));   // wild 16-byte store, inside the oend-32 margin
-    }
+    st16(L.dst + op, window_shift1(w));   // wild 16-byte store, inside the oend-32 margin
 }
 
 // Match that starts inside the external dictionary (lz4.c:2252-2277).
@@ -478,9 +297,9 @@ __device__ __noinline__ void dict_match(Lane& L, int64_t op, int64_t off, int64_
 }
 
 // One sequence of block L.  Deferred copies land in lc / mc.
-template <bool DICT, bool STAGE>
+template <bool DICT>
 __device__ __forceinline__ void decode_step(Lane& L, Copy& lc, Copy& mc) {
-    const u32x4 w = in16<STAGE>(L, L.ip);
+    const u32x4 w = in16(L, L.ip);
     const uint32_t tok = w.x & 0xFFu;
     int64_t ip = L.ip + 1;
     int64_t op = L.op;
@@ -493,32 +312,32 @@ __device__ __forceinline__ void decode_step(Lane& L, Copy& lc, Copy& mc) {
 
     if (L.fast) {   // lz4.c:1996-2109
         if (lit == 15) {
-            if (!read_len<STAGE>(L, ip, iend - 15, true, add)) goto fail;
+            if (!read_len(L, ip, iend - 15, true, add)) goto fail;
             lit += add;
             if (op + lit > oend - 32 || ip + lit > iend - 32) {
                 L.fast = false;
                 goto literal_tail;
             }
-            emit_literal<STAGE>(L, ip, op, lit, lc, false);
+            emit_literal(L, ip, op, lit, lc, false);
             deferred = lc.kind != kNone;
             ip += lit;
             op += lit;
-            off = in_le16<STAGE>(L, ip);
+            off = in_le16(L, ip);
         } else {
             if (ip > iend - 17) {
                 L.fast = false;
                 goto literal_tail;
             }
             // literals are bytes 1..lit of the token window
-            window_literal<STAGE>(L, op, w, lit);
-            off = lit <= 13 ? (window_dword(w, (uint32_t)(1 + lit)) & 0xFFFFu) : in_le16<STAGE>(L, ip + lit);
+            window_literal(L, op, w, lit);
+            off = lit <= 13 ? (window_dword(w, (uint32_t)(1 + lit)) & 0xFFFFu) : in_le16(L, ip + lit);
             ip += lit;
             op += lit;
         }
         ip += 2;
         ml = tok & 15;
         if (ml == 15) {
-            if (!read_len<STAGE>(L, ip, iend - 4, false, add)) goto fail;
+            if (!read_len(L, ip, iend - 4, false, add)) goto fail;
             ml += add + 4;
             if (OOW(off)) goto fail;
             if (op + ml >= oend - 64) {
@@ -532,7 +351,7 @@ __device__ __forceinline__ void decode_step(Lane& L, Copy& lc, Copy& mc) {
                 goto match_tail;
             }
             if (off >= 8 && off <= op) {
-                emit_match<STAGE>(L, op, off, ml, mc, deferred);
+                emit_match(L, op, off, ml, mc, deferred);
                 op += ml;
                 goto done;
             }
@@ -545,53 +364,49 @@ __device__ __forceinline__ void decode_step(Lane& L, Copy& lc, Copy& mc) {
             op += ml;
             goto done;
         }
-        emit_match<STAGE>(L, op, off, ml, mc, deferred);
+        emit_match(L, op, off, ml, mc, deferred);
         op += ml;
         goto done;
     }
 
     // safe phase, lz4.c:2114-2329
     if (lit != 15 && ip < iend - 16 && op <= oend - 32) {   // shortcut, lz4.c:2128-2158
-        window_literal<STAGE>(L, op, w, lit);
-        off = lit <= 13 ? (window_dword(w, (uint32_t)(1 + lit)) & 0xFFFFu) : in_le16<STAGE>(L, ip + lit);
+        window_literal(L, op, w, lit);
+        off = lit <= 13 ? (window_dword(w, (uint32_t)(1 + lit)) & 0xFFFFu) : in_le16(L, ip + lit);
         op += lit;
         ip += lit + 2;
         ml = tok & 15;
         if (ml != 15 && off >= 8 && off <= op) {
-            if (STAGE) {
-                stage_match(L, op, off, ml + 4);
-            } else {
-                lane_match(L.dst + op, off, ml + 4, oend - op);
-            }
+            lane_match(L.dst + op, off, ml + 4, oend - op);
             op += ml + 4;
             goto done;
         }
         goto match_length;
     }
     if (lit == 15) {
-        if (!read_len<STAGE>(L, ip, iend - 15, true, add)) goto fail;
+        if (!read_len(L, ip, iend - 15, true, add)) goto fail;
         lit += add;
     }
 literal_tail:   // lz4.c:2172-2229
     if (op + lit > oend - 12 || ip + lit > iend - 8) {
         if (ip + lit != iend || op + lit > oend) goto fail;
-        emit_literal<STAGE>(L, ip, op, lit, lc, false);   // last literals: exact (never past oend / iend)
+        emit_literal(L, ip, op, lit, lc, false);   // last literals: exact (never past oend / iend)
         op += lit;
         L.result = (int32_t)op;
         L.live = false;
         L.op = op;
         return;
     }
-    emit_literal<STAGE>(L, ip, op, lit, lc, false);
+    emit_literal(L, ip, op, lit, lc, false);
     deferred = lc.kind != kNone;
     ip += lit;
     op += lit;
-    off = in_le16<STAGE>(L, ip);
+    off = in_le16(L, ip);
     ip += 2;
     ml = tok & 15;
 match_length:   // lz4.c:2238-2245
     if (ml == 15) {
-        if (!read_len<STAGE>(L, ip, iend - 4, false, add)) goto fail;
+        if (!read_len(L, ip, iend - 4, false, add)) goto fail;
         ml += add;
     }
     ml += 4;
@@ -605,7 +420,7 @@ match_tail:   // lz4.c:2248-2328
         goto done;
     }
     if (op + ml > oend - 5) goto fail;
-    emit_match<STAGE>(L, op, off, ml, mc, deferred);
+    emit_match(L, op, off, ml, mc, deferred);
     op += ml;
 done:
     L.ip = ip;
@@ -674,7 +489,7 @@ __global__ __launch_bounds__(256) void decompress_kernel(const uint8_t* __restri
 
     while (__any(L.live)) {
         Copy lc{kNone, 0, 0, 0}, mc{kNone, 0, 0, 0};
-        if (L.live) decode_step<DICT, false>(L, lc, mc);
+        if (L.live) decode_step<DICT>(L, lc, mc);
         uint64_t pend = __ballot(lc.kind != kNone || mc.kind != kNone);
         if (pend == 0) continue;
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // lane stores visible to the wave
@@ -707,194 +522,6 @@ __global__ __launch_bounds__(256) void decompress_kernel(const uint8_t* __restri
 }
 
 
-// One round of wave-cooperative long copies in STAGE mode.  Each lane with
-// a copy [dpos, E) first writes the head up to the next 64-byte boundary A
-// through its stage and flushes, so [0, A) is in HBM; the wave then copies
-// [A, E) of every such lane straight to HBM at wave width (lane order); the
-// lane finally restarts its stage from HBM at E.
-__device__ __forceinline__ void stage_coop(Lane& L, const Copy& c, uint32_t lane) {
-    int64_t A = 0, E = 0;
-    bool coop = false;
-    if (c.kind != kNone) {
-        E = c.dpos + c.len;
-        const int64_t up = (c.dpos + 63) & ~(int64_t)63;
-        A = up < E ? up : E;
-        if (A > c.dpos) {
-            if (c.kind == kLiteral) {
-                stage_literal(L, c.dpos, c.arg, A - c.dpos);
-            } else {
-                stage_match(L, c.dpos, c.arg, A - c.dpos);
-            }
-        }
-        if (A < E) {
-            while (L.F + 64 <= A) stage_flush(L);
-            coop = true;
-        }
-    }
-    uint64_t pend = __ballot(coop);
-    if (pend == 0) return;
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // flushed heads visible to the wave
-    while (pend) {
-        const int l = __builtin_ctzll(pend);
-        pend &= pend - 1;
-        uint8_t* d = readlane_ptr(L.dst, l);
-        const int64_t oend = readlane64(L.oend, l);
-        const int64_t a = readlane64(A, l), e = readlane64(E, l);
-        if (__builtin_amdgcn_readlane(c.kind, l) == kLiteral) {
-            const uint8_t* s = readlane_ptr(L.src, l);
-            const int64_t iend = readlane64(L.iend, l);
-            const int64_t sp = readlane64(c.arg, l) + (a - readlane64(c.dpos, l));
-            wave_literal<1>(d + a, s + sp, e - a, oend - a, iend - sp, lane);
-        } else {
-            wave_match(d + a, readlane64(c.arg, l), e - a, oend - a, lane);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-    }
-    if (coop) stage_reload(L, E);
-}
-
-// ---------------------------------------------------------------- fast path
-// The common sequence, in the reference's fast loop (lz4.c:1996-2109):
-// literal length <= 12 (literal and offset inside the 16-byte token window),
-// at most one extra match-length byte, offset >= 16 and within the output,
-// match <= 64 bytes, and both the literal and the match take the in-loop
-// branches (ip <= iend - 17 after the token; op + ml < oend - 64; the
-// match-length read stays below iend - 4).  Such a sequence cannot fail and
-// is decoded exactly as decode_step would; anything else takes decode_step.
-struct FastSeq {
-    int64_t lit, off, ml, ipn;
-};
-
-__device__ __forceinline__ bool fast_seq(const Lane& L, u32x4 w, FastSeq& f) {
-    const uint32_t tok = w.x & 0xFFu;
-    const int64_t lit = tok >> 4, mlc = tok & 15;
-    const int64_t ip1 = L.ip + 1;
-    if (!L.fast || lit > 12 || ip1 > L.iend - 17) return false;
-    const int64_t off = window_dword(w, (uint32_t)(1 + lit)) & 0xFFFFu;
-    int64_t ml = mlc + 4, ipn = ip1 + lit + 2;
-    if (mlc == 15) {   // read_len (lz4.c:1903-1928) with a single byte < 255
-        const int64_t b = byte_of(w, (int)(3 + lit));
-        if (b == 255 || ipn + 1 > L.iend - 4) return false;
-        ml = 19 + b;
-        ipn += 1;
-    }
-    const int64_t opm = L.op + lit;
-    if (off < 16 || off > opm || ml > kCoopMin || opm + ml >= L.oend - 64) return false;
-    f = FastSeq{lit, off, ml, ipn};
-    return true;
-}
-
-__device__ __forceinline__ void fast_exec(Lane& L, u32x4 w, const FastSeq& f) {
-    lds_st16(stage_at(L, L.op), window_shift1(w));   // literals (wild), op < F + 64
-    const int64_t opm = L.op + f.lit;
-    for (int64_t i = 0; i < f.ml; i += 16) {
-        stage_sync(L, opm + i);
-        lds_st16(stage_at(L, opm + i), out_read16(L, opm + i - f.off));
-    }
-    L.ip = f.ipn;
-    L.op = opm + f.ml;
-}
-
-// Independent blocks without a dictionary (the hot path): one lane per block,
-// LDS-staged input and output.  Each iteration every live lane classifies its
-// next sequence; the wave runs a fast step for the fast-path lanes, or -- once
-// `slow_batch` lanes wait (or none can go fast) -- one general decode_step
-// for the waiting lanes.  Batching keeps the rarely needed general state
-// machine (and its divergence) off most iterations.
-// 4 waves per SIMD (<= 128 VGPRs): the LDS allows 16 waves per CU
-__global__ __launch_bounds__(256, 4) void stage_decompress_kernel(const uint8_t* __restrict__ src,
-                                                               const int64_t* __restrict__ src_off,
-                                                               const int32_t* __restrict__ src_len, uint8_t* dst,
-                                                               const int64_t* __restrict__ dst_off,
-                                                               const int32_t* __restrict__ dst_cap,
-                                                               int32_t* __restrict__ status, int64_t n,
-                                                               unsigned long long* __restrict__ next,
-                                                               int32_t slow_batch) {
-    __shared__ __attribute__((aligned(16))) uint8_t stages[256 * kStage];
-    __shared__ __attribute__((aligned(16))) uint8_t wins[256 * kWin];
-    const uint32_t lane = lane_id();
-    Lane L;
-    L.live = false;
-    L.result = -1;
-    L.stage = (lds_u8*)(stages + threadIdx.x * kStage);
-    L.win = (lds_u8*)(wins + threadIdx.x * kWin);
-    L.ip = 0;
-    L.op = 0;
-    L.F = 0;
-    L.ib = 0;
-    L.dict_len = 0;
-    L.dict_end = nullptr;
-    int64_t idx = -1;    // block this lane decodes
-    bool more = true;    // wave-uniform: the queue may still hold blocks
-    while (true) {
-        // idle lanes take the next blocks: one atomic per wave and refill
-        if (more) {
-            const uint64_t need = __ballot(!L.live);
-            if (need != 0) {
-                const int first = __builtin_ctzll(need);
-                const uint32_t cnt = (uint32_t)__popcll(need);
-                unsigned long long base = 0;
-                if ((int)lane == first) base = atomicAdd(next, (unsigned long long)cnt);
-                base = (unsigned long long)readlane64((int64_t)base, first);
-                if (base + cnt >= (unsigned long long)n) more = false;
-                if (!L.live) {
-                    const uint64_t below = lane == 0 ? 0 : (need & (~0ull >> (64 - lane)));
-                    idx = (int64_t)(base + (unsigned long long)__popcll(below));
-                    if (idx < n) {
-                        L.src = src + src_off[idx];
-                        L.dst = dst + dst_off[idx];
-                        L.iend = src_len[idx];
-                        L.oend = dst_cap[idx];
-                        L.ip = 0;
-                        L.op = 0;
-                        L.F = 0;
-                        L.ib = -2 * kWin;
-                        if (L.oend < 0) {
-                            status[idx] = -1;   // lz4.c:1950
-                        } else if (L.oend == 0) {
-                            status[idx] = (L.iend == 1 && L.src[0] == 0) ? 0 : -1;   // lz4.c:1978-1982
-                        } else if (L.iend <= 0) {
-                            status[idx] = -1;   // lz4.c:1983
-                        } else {
-                            L.fast = L.oend >= 64;
-                            L.live = true;
-                        }
-                    }
-                }
-            }
-        }
-        if (!__any(L.live)) {
-            if (more) continue;
-            break;
-        }
-        FastSeq f{0, 0, 0, 0};
-        u32x4 w = u32x4{0, 0, 0, 0};
-        bool fok = false;
-        if (L.live) {
-            win_sync(L);
-            stage_sync(L, L.op);
-            w = lds_ld16(L.win + (L.ip - L.ib));
-            fok = fast_seq(L, w, f);
-        }
-        const uint64_t fm = __ballot(fok);
-        const uint64_t sm = __ballot(L.live && !fok);
-        if (sm != 0 && (fm == 0 || __popcll(sm) >= (uint32_t)slow_batch)) {
-            Copy lc{kNone, 0, 0, 0}, mc{kNone, 0, 0, 0};
-            const bool stepped = L.live && !fok;
-            if (stepped) decode_step<false, true>(L, lc, mc);
-            if (__ballot(lc.kind != kNone || mc.kind != kNone)) {
-                stage_coop(L, lc, lane);   // literal before match
-                stage_coop(L, mc, lane);
-            }
-            if (stepped && !L.live) {   // block finished (or failed)
-                stage_finish(L, L.result >= 0 ? (int64_t)L.result : L.op);
-                status[idx] = L.result;
-            }
-        } else if (fok) {
-            fast_exec(L, w, f);
-        }
-    }
-}
 
 // ------------------------------------------------- cooperative (small batches)
 // One wavefront per block, for batches too small to fill the lane decoder
@@ -1050,7 +677,7 @@ __device__ __forceinline__ int32_t coop_finish(const uint8_t* s, uint8_t* d, int
     }
     while (__any(L.live)) {
         Copy lc{kNone, 0, 0, 0}, mc{kNone, 0, 0, 0};
-        if (L.live) decode_step<DICT, false>(L, lc, mc);
+        if (L.live) decode_step<DICT>(L, lc, mc);
         if (__ballot(lc.kind != kNone || mc.kind != kNone) == 0) continue;
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
         const int64_t oe = readlane64(L.oend, 0);
@@ -1071,147 +698,6 @@ __device__ __forceinline__ int32_t coop_finish(const uint8_t* s, uint8_t* d, int
         }
     }
     return __builtin_amdgcn_readlane(L.result, 0);
-}
-
-__global__ __launch_bounds__(256) void coop_decompress_kernel(const uint8_t* __restrict__ src,
-                                                              const int64_t* __restrict__ src_off,
-                                                              const int32_t* __restrict__ src_len, uint8_t* dst,
-                                                              const int64_t* __restrict__ dst_off,
-                                                              const int32_t* __restrict__ dst_cap,
-                                                              int32_t* __restrict__ status, int64_t n) {
-    __shared__ __attribute__((aligned(16))) uint8_t ins[4][kCoopIn + 64];
-    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    lds_u8* IN = (lds_u8*)ins[wv];
-    // static assignment (an atomic work queue in this loop nest compiled to
-    // a kernel that hung, tools/micro/coop_decode.hip)
-    for (int64_t b = (int64_t)blockIdx.x * 4 + wv; b < n; b += (int64_t)gridDim.x * 4) {
-        const uint8_t* s = src + src_off[b];
-        uint8_t* d = dst + dst_off[b];
-        const int32_t iend = src_len[b], oend = dst_cap[b];
-        if (oend < 0 || iend <= 0 || oend == 0) {   // lz4.c:1950, :1978-1983
-            if (lane == 0) status[b] = (oend == 0 && iend == 1 && s[0] == 0) ? 0 : -1;
-            continue;
-        }
-        const bool fast = oend >= 64;
-        int32_t ip = 0, op = 0;
-        while (fast) {
-            const int32_t ib = ip & ~15;
-            {
-                const int32_t x = ib + 16 * (int32_t)lane;
-                const u32x4 v = x + 16 <= iend ? ld16(s + x) : ld16_guarded(s + x, iend - x);
-                lds_st16(IN + 16 * lane, v);
-            }
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-            // speculative parse + walk: lane k gets the k-th sequence start
-            int32_t myseq = 0;
-            int nseq = 0;
-            bool stop = false;
-            int32_t pos = ip - ib;
-            while (nseq < 64 && pos + 80 <= kCoopIn) {
-                const CoopSeq q = coop_parse(IN, pos + (int32_t)lane, lds_ld16(IN + pos + (int32_t)lane));
-                const bool simple = q.simple;
-                const int32_t nxt = (int32_t)lane + q.adv;
-                const uint64_t smask = __ballot(simple);
-                int32_t sidx = 0;
-                while (sidx < 64 && nseq < 64) {
-                    if (!((smask >> sidx) & 1ull)) {
-                        stop = true;
-                        break;
-                    }
-                    if ((int)lane == nseq) myseq = pos + sidx;
-                    ++nseq;
-                    sidx = __builtin_amdgcn_readlane(nxt, sidx);
-                }
-                pos += sidx;
-                if (stop) break;
-            }
-            if (nseq == 0) {
-                // one sequence with literal > 12 bytes (or a long length), whole wave
-                const uint32_t tok = s[ip];
-                int32_t lit = (int32_t)(tok >> 4), ml = (int32_t)(tok & 15u), q = ip + 1;
-                if (lit == 15) {
-                    uint32_t x = 255;
-                    while (x == 255 && q < iend - 48) {
-                        x = s[q++];
-                        lit += (int32_t)x;
-                    }
-                    if (x == 255 || q + lit > iend - 32 || op + lit > oend - 32) break;   // lz4.c:2016-2027
-                } else if (q > iend - 17) {
-                    break;   // lz4.c:2034
-                }
-                const int32_t opm = op + lit;
-                const int32_t off = (int32_t)s[q + lit] | ((int32_t)s[q + lit + 1] << 8);
-                int32_t qe = q + lit + 2;
-                if (ml == 15) {
-                    uint32_t x = 255;
-                    while (x == 255 && qe < iend - 5) {
-                        x = s[qe++];
-                        ml += (int32_t)x;
-                    }
-                    if (x == 255 || qe > iend - 5) break;
-                }
-                ml += 4;
-                if (off < 1 || off > opm || opm + ml >= oend - 64) break;
-                coop_copy_literal(d + op, s + q, lit, lane);
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-                coop_copy_match(d + opm, off, ml, lane);
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-                op = opm + ml;
-                ip = qe;
-                continue;
-            }
-            // sequence k in lane k
-            const bool act = (int)lane < nseq;
-            const int32_t tk = act ? myseq : 0;
-            const u32x4 w = lds_ld16(IN + tk);
-            const CoopSeq q = coop_parse(IN, tk, w);
-            const int32_t lit = q.lit, off = q.off, ml = q.ml, adv = q.adv;
-            const int32_t len = act ? lit + ml : 0;
-            const int32_t o = op + coop_incl_sum(len) - len;
-            const int32_t sabs = ib + myseq;
-            // the reference's fast-loop margins (lz4.c:2004-2110, as fast_seq / decode_step)
-            const bool lit_ok = q.litx ? ib + q.litpos + lit <= iend - 32 && o + lit <= oend - 32
-                                       : sabs + 1 <= iend - 17;
-            const bool ok = act && q.simple && lit_ok && (!q.mlx || sabs + adv <= iend - 4) && off >= 1 &&
-                            off <= o + lit && o + len < oend - 64;
-            const uint64_t bad = __ballot(act) & ~__ballot(ok);
-            const int use = bad ? __builtin_ctzll(bad) : nseq;
-            if (use == 0) break;
-            const bool u = (int)lane < use;
-            if (u && lit > 0) {
-                if (lit <= 12) {
-                    put_exact(d + o, window_shift1(w), (uint32_t)lit);
-                } else {
-                    for (int32_t i = 0; i < lit; i += 16) coop_put(d + o + i, lds_ld16(IN + q.litpos + i), lit - i);
-                }
-            }
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-            const int32_t m = o + lit;
-            const int32_t src_end = m - off + (off < ml ? off : ml);
-            uint64_t pend = __ballot(u);
-            while (pend) {
-                const int32_t E = __builtin_amdgcn_readlane(m, __builtin_ctzll(pend));
-                const bool ready = ((pend >> lane) & 1ull) && src_end <= E;
-                if (ready) {
-                    if (off >= 16) {
-                        for (int32_t i = 0; i < ml; i += 16) coop_put(d + m + i, ld16(d + m - off + i), ml - i);
-                    } else {
-                        const u32x4 pat = period_pattern(ld16(d + m - off), (uint32_t)off);
-                        const int32_t step = 16 - (16 % off);
-                        for (int32_t i = 0; i < ml; i += step) coop_put(d + m + i, pat, ml - i);
-                    }
-                }
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-                pend &= ~__ballot(ready);
-            }
-            op = __builtin_amdgcn_readlane(o + len, use - 1);
-            ip = ib + __builtin_amdgcn_readlane(myseq + adv, use - 1);
-            if (use < nseq) break;
-        }
-        // the rest with the exact state machine on lane 0, long copies on the wave
-        const int32_t r = coop_finish(s, d, iend, oend, ip, op, fast, lane);
-        if (lane == 0) status[b] = r;
-    }
 }
 
 // ------------------------------------ cooperative with on-chip history
@@ -1585,7 +1071,7 @@ __global__ __launch_bounds__(64) void decompress_chain_kernel(const uint8_t* __r
         }
         while (__any(L.live)) {
             Copy lc{kNone, 0, 0, 0}, mc{kNone, 0, 0, 0};
-            if (L.live) decode_step<true, false>(L, lc, mc);
+            if (L.live) decode_step<true>(L, lc, mc);
             const uint64_t pend = __ballot(lc.kind != kNone || mc.kind != kNone);
             if (pend == 0) continue;
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
@@ -1630,43 +1116,24 @@ int current_device() {
     return dev >= 0 && dev < 64 ? dev : 0;
 }
 
-// Persistent grid for the staged decoder: every resident workgroup slot of
-// the device, no more (blocks come from the work queue).  Cached per device.
-int64_t stage_grid(int64_t n) {
-    static std::atomic<int64_t> cache[64];
-    const int dev = current_device();
-    int64_t slots = cache[dev].load(std::memory_order_relaxed);
-    if (slots == 0) {
-        int cus = 0, per_cu = 0;
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(lz4m::stage_decompress_kernel),
-                                                           256, 0);
-        slots = (int64_t)(cus > 0 ? cus : 256) * (per_cu > 0 ? per_cu : 1);
-        cache[dev].store(slots, std::memory_order_relaxed);
-    }
-    const int64_t need = (n + 255) / 256;
-    return need < slots ? need : slots;
-}
-
 int env_int(const char* name, int dflt) {
     const char* e = getenv(name);
     const int v = e != nullptr ? atoi(e) : 0;
     return v > 0 ? v : dflt;
 }
 
-enum Decoder { kAuto = 0, kLaneDec, kCoopDec, kHistDec, kRowsDec, kDirectDec, kQuadDec };
+// the values are the C-ABI's decoder ids (include/lz4m.h); 1, 2 and 5 were
+// retired decoders and are rejected
+enum Decoder { kAuto = 0, kHistDec = 3, kRowsDec = 4, kQuadDec = 6 };
 
-// LZ4M_DECODER forces a decoder (A/B measurements, tests): lane | hist | coop |
-// rows | direct; unset = by batch size and scratch.
+// LZ4M_DECODER forces a decoder (A/B measurements, tests): hist | rows |
+// quad; unset = by batch size and scratch.
 int decoder_env() {
     static const int mode = [] {
         const char* e = getenv("LZ4M_DECODER");
         if (e == nullptr) return (int)kAuto;
-        if (strcmp(e, "lane") == 0) return (int)kLaneDec;
-        if (strcmp(e, "coop") == 0) return (int)kCoopDec;
         if (strcmp(e, "hist") == 0) return (int)kHistDec;
         if (strcmp(e, "rows") == 0) return (int)kRowsDec;
-        if (strcmp(e, "direct") == 0) return (int)kDirectDec;
         if (strcmp(e, "quad") == 0) return (int)kQuadDec;
         return (int)kAuto;
     }();
@@ -1687,31 +1154,21 @@ extern "C" int lz4m_decompress_batch_sel(const uint8_t* d_src, const int64_t* d_
                                          uint8_t* d_dst, const int64_t* d_dst_off, const int32_t* d_dst_cap,
                                          int32_t* d_status, int64_t n, void* d_work, size_t work_bytes, int decoder,
                                          lz4m_stream_t stream) {
-    if (n < 0 || decoder < 0 || decoder > kQuadDec) return LZ4M_EINVAL;
+    if (n < 0 || !(decoder == kAuto || decoder == kHistDec || decoder == kRowsDec || decoder == kQuadDec))
+        return LZ4M_EINVAL;
     if (n == 0) return 0;
     hipStream_t st = (hipStream_t)stream;
     if (decoder == kAuto) decoder = decoder_env();
-    if (decoder == kDirectDec) {
-        const int64_t grid = (n + 255) / 256;
-        hipLaunchKernelGGL(decompress_kernel<false>, dim3((uint32_t)grid), dim3(256), 0, st, d_src, d_src_off,
-                           d_src_len, d_dst, d_dst_off, d_dst_cap, nullptr, nullptr, nullptr, d_status, n, nullptr);
-        return (int)hipGetLastError();
-    }
     if (d_work == nullptr || work_bytes < lz4m_decompress_workspace_bytes() || ((uintptr_t)d_work & 7) != 0)
         return LZ4M_EINVAL;
     // the large-batch decoder needs scratch for its per-block records and
-    // sequence lengths (lz4m_decompress_workspace_size)
+    // sequence lengths (lz4m_decompress_workspace_size); without it (or for
+    // small batches) the one-wavefront-per-block decoder takes any batch
     const bool rows_fit = work_bytes >= lz4m_rows_fixed_bytes(n) + 64;
     // LZ4M_ROWS_MIN_BLOCKS: smallest batch sent to the row decoder (tuning)
     static const int rows_min = env_int("LZ4M_ROWS_MIN_BLOCKS", 32768);   // crossover measured, DESIGN 3.1
-    // LZ4M_COOP_MAX_BLOCKS: largest batch sent to the one-wave-per-block decoder
-    static const int coop_max = env_int("LZ4M_COOP_MAX_BLOCKS", 98304);
-    if (decoder == kAuto) {
-        if (rows_fit && n >= rows_min) decoder = kRowsDec;
-        else if (n <= coop_max) decoder = kHistDec;
-        else decoder = kLaneDec;
-    }
-    if ((decoder == kRowsDec || decoder == kQuadDec) && !rows_fit) decoder = n <= coop_max ? kHistDec : kLaneDec;
+    if (decoder == kAuto) decoder = rows_fit && n >= rows_min ? kRowsDec : kHistDec;
+    if (decoder != kHistDec && !rows_fit) decoder = kHistDec;
     if (decoder == kRowsDec || decoder == kQuadDec) {
         const int quad = decoder == kQuadDec;
         int pg = 1, eg = 1;
@@ -1725,24 +1182,9 @@ extern "C" int lz4m_decompress_batch_sel(const uint8_t* d_src, const int64_t* d_
                            d_src_len, d_dst, d_dst_off, d_dst_cap, nullptr, nullptr, nullptr, d_status, n, meta);
         return (int)hipGetLastError();
     }
-    if (decoder == kHistDec || decoder == kCoopDec) {
-        const int64_t grid = (n + 3) / 4;
-        const dim3 g((uint32_t)(grid < 65536 ? grid : 65536));
-        if (decoder == kHistDec)   // the on-chip-history kernel; kCoopDec: the HBM-only one (A/B)
-            hipLaunchKernelGGL(hist_decompress_kernel<false>, g, dim3(256), 0, st, d_src, d_src_off, d_src_len, d_dst,
-                               d_dst_off, d_dst_cap, d_status, n, nullptr, (int64_t)0);
-        else
-            hipLaunchKernelGGL(coop_decompress_kernel, g, dim3(256), 0, st, d_src, d_src_off, d_src_len, d_dst,
-                               d_dst_off, d_dst_cap, d_status, n);
-        return (int)hipGetLastError();
-    }
-    // LZ4M_SLOW_BATCH: waiting lanes that trigger a general step (tuning)
-    static const int slow_batch = env_int("LZ4M_SLOW_BATCH", 6);
-    hipError_t e = hipMemsetAsync(d_work, 0, sizeof(unsigned long long), st);
-    if (e != hipSuccess) return (int)e;
-    hipLaunchKernelGGL(stage_decompress_kernel, dim3((uint32_t)stage_grid(n)), dim3(256), 0, st, d_src, d_src_off,
-                       d_src_len, d_dst, d_dst_off, d_dst_cap, d_status, n, static_cast<unsigned long long*>(d_work),
-                       slow_batch);
+    const int64_t grid = (n + 3) / 4;
+    hipLaunchKernelGGL(hist_decompress_kernel<false>, dim3((uint32_t)(grid < 65536 ? grid : 65536)), dim3(256), 0, st,
+                       d_src, d_src_off, d_src_len, d_dst, d_dst_off, d_dst_cap, d_status, n, nullptr, (int64_t)0);
     return (int)hipGetLastError();
 }
 
@@ -1759,15 +1201,12 @@ extern "C" int lz4m_decompress_batch(const uint8_t* d_src, const int64_t* d_src_
                                      int32_t* d_status, int64_t n, lz4m_stream_t stream) {
     if (n < 0) return LZ4M_EINVAL;
     if (n == 0) return 0;
-    // stream-ordered scratch for this call only (the work-queue counter of
-    // the lane decoder): no state is shared between calls in flight
-    void* work = nullptr;
-    hipError_t e = hipMallocAsync(&work, 64, (hipStream_t)stream);
-    if (e != hipSuccess) return (int)e;
-    const int rc = lz4m_decompress_batch_sel(d_src, d_src_off, d_src_len, d_dst, d_dst_off, d_dst_cap, d_status, n,
-                                             work, 64, kAuto, stream);
-    e = hipFreeAsync(work, (hipStream_t)stream);
-    return rc != 0 ? rc : (int)e;
+    // no scratch: the one-wavefront-per-block decoder (any batch size)
+    const int64_t grid = (n + 3) / 4;
+    hipLaunchKernelGGL(hist_decompress_kernel<false>, dim3((uint32_t)(grid < 65536 ? grid : 65536)), dim3(256), 0,
+                       (hipStream_t)stream, d_src, d_src_off, d_src_len, d_dst, d_dst_off, d_dst_cap, d_status, n,
+                       nullptr, (int64_t)0);
+    return (int)hipGetLastError();
 }
 
 extern "C" int lz4m_decompress_batch_dict(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len,

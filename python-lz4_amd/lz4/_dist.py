@@ -108,49 +108,199 @@ def gather_compressed(comp: torch.Tensor, block_len: torch.Tensor, root: int = 0
     return gather_finish(gather_start(comp, block_len, root, group))
 
 
+class _Side:
+    """The side stream the gather runs on (GPU tensors): high priority, so its
+    copies and the RCCL launches it orders are not queued behind compression
+    kernels.  Collectives posted under it make RCCL's stream wait only for
+    what was recorded here (torch's ProcessGroupNCCL syncs with the *current*
+    stream), i.e. for the wave being gathered, not for the next wave's
+    compression enqueued after it.  With CPU tensors (gloo) it is a no-op."""
+
+    def __init__(self, dev: torch.device):
+        self.gpu = dev.type == "cuda"
+        self.stream = torch.cuda.Stream(device=dev, priority=-1) if self.gpu else None
+
+    def ctx(self):
+        return torch.cuda.stream(self.stream) if self.gpu else _Null()
+
+    def mark(self):
+        """An event after everything enqueued on the current stream so far (None on CPU)."""
+        if not self.gpu:
+            return None
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.stream.device))
+        return ev
+
+    def wait(self, ev):
+        """Order the side stream after `ev`."""
+        if ev is not None:
+            self.stream.wait_event(ev)
+
+    def before_current(self):
+        """Order the current stream after everything enqueued on the side stream so far."""
+        if self.gpu:
+            torch.cuda.current_stream(self.stream.device).wait_stream(self.stream)
+
+
+class _Null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+def _page_bounds(lens: torch.Tensor, page_blocks: int) -> torch.Tensor:
+    """Byte offsets of the page cuts of one shard: page k = blocks
+    [k * page_blocks, (k + 1) * page_blocks); returns int64 [pages + 1]."""
+    n = lens.numel()
+    csum = torch.zeros(n + 1, dtype=torch.int64, device=lens.device)
+    if n:
+        torch.cumsum(lens.to(torch.int64), 0, out=csum[1:])
+    pages = (n + page_blocks - 1) // page_blocks
+    idx = (torch.arange(pages + 1, device=lens.device) * page_blocks).clamp_(max=n)
+    return csum[idx]
+
+
 def compress_gather_waves(compress_wave, waves: int, root: int = 0, group=None, overlap: bool = True,
-                          consume=None) -> dict:
+                          consume=None, page_blocks: int = 4096, ring: int = 4) -> dict:
     """Config 5's wave driver: a shard larger
     than HBM is compressed in `waves` waves over a resident working set, and
-    every wave's compressed output is gathered at `root`.
+    every wave's compressed output is gathered at `root`, which consumes it
+    page by page (a root cannot hold 8 ranks' waves: at 1 M x 64 KiB blocks
+    a wave is ~34 GiB compressed per rank).
 
     compress_wave(w) -> (comp uint8 1-D, block_len int32 1-D): enqueues wave
-    w's compression + compaction on the current stream and returns its
-    compacted output (the buffers must stay valid until the wave after next
-    is requested: double-buffer them).  With `overlap`, the gather of wave w
-    runs while wave w + 1 compresses (the bulk transfers are posted before
-    the next wave is enqueued).  consume(w, buf, offsets, lengths) is called
-    on the root with each gathered wave.  Returns byte counts for rates.
+    w's compression + compaction on the current stream and returns the
+    compacted blocks, back to back (comp may be longer than the blocks).
+    The driver calls compress_wave(w + 2) only after wave w's transfers out
+    of its buffers are ordered before the current stream, so two buffers
+    alternated by w & 1 are enough.
+
+    consume(w, src_rank, first_block, buf, lens) is called on the root for
+    every page: `lens` (int32, device) are the sizes of blocks
+    first_block .. first_block + len(lens) of rank src_rank's wave w, back to
+    back in `buf`.  On GPU tensors it is called under the gather's side
+    stream and must only enqueue work there; `buf` is valid only during the
+    call's stream work (the memory is reused for a later page), so clone it
+    to keep it.
+
+    Per wave: the root learns every rank's page sizes from two small
+    all_gathers (block counts, then block sizes) -- the one host wait per
+    wave, needed because point-to-point sizes must be known on the host.
+    With `overlap` (default) wave w's gather is posted only after wave w + 1's
+    compression is enqueued, so that wait lands while the GPU compresses and
+    the transfers run beside the next wave; without it each wave's gather
+    completes before the next wave starts.  Peers send their pages with
+    isend; the root receives them into a ring of `ring` page buffers per peer
+    and consumes its own shard in place.  Returns byte counts for rates.
     """
     rank = dist.get_rank(group)
-    bufs = [None, None]
-    stats = {"waves": waves, "comp_bytes": 0, "gathered_bytes": 0, "blocks": 0}
+    world = dist.get_world_size(group)
+    stats = {"waves": waves, "comp_bytes": 0, "gathered_bytes": 0, "blocks": 0, "pages": 0, "host_waits": 0}
+    side = None
+    sends = {}            # wave -> outstanding send works (buffers of that wave in use)
+    slots = {}            # (peer, ring index) -> receive buffer
     pending = None
 
-    def done(w, h):
-        buf, off, lens = gather_finish(h)
-        if rank == root:
-            stats["gathered_bytes"] += buf.numel()
-            if consume is not None:
-                consume(w, buf, off, lens)
-            bufs[w & 1] = buf
+    def post(w, comp, lens, ev):
+        dev = comp.device
+        side.wait(ev)                 # wave w's compression, not the next wave's
+        with side.ctx():
+            meta = torch.tensor([lens.numel()], dtype=torch.int64, device=dev)
+            metas = [torch.empty_like(meta) for _ in range(world)]
+            dist.all_gather(metas, meta, group=group)
+            counts = [int(x) for x in torch.cat(metas).cpu()]          # host wait (1)
+            mx = max(counts)
+            padded = torch.zeros(mx, dtype=torch.int32, device=dev)
+            padded[: lens.numel()] = lens
+            lens_all = [torch.empty(mx, dtype=torch.int32, device=dev) for _ in range(world)]
+            dist.all_gather(lens_all, padded, group=group)
+            lens_all = [lens_all[r][: counts[r]] for r in range(world)]
+            need = range(world) if rank == root else [rank]
+            bounds = {r: _page_bounds(lens_all[r], page_blocks) for r in need}
+            hb = torch.cat([bounds[r] for r in need]).cpu().tolist()    # host wait (2), same sync point
+            stats["host_waits"] += 2
+            pos = 0
+            host_bounds = {}
+            for r in need:
+                k = bounds[r].numel()
+                host_bounds[r] = hb[pos: pos + k]
+                pos += k
+            mine = host_bounds[rank]
+            stats["comp_bytes"] += mine[-1]
+            stats["blocks"] += lens.numel()
+            if rank != root:
+                works = []
+                for k in range(len(mine) - 1):
+                    a, b = mine[k], mine[k + 1]
+                    if b > a:
+                        works.append(dist.isend(comp[a:b], dst=_global(root, group), group=group))
+                        stats["pages"] += 1
+                sends[w] = works
+                return
+            # root: own shard in place, then every peer's pages through the ring
+            for k in range(len(mine) - 1):
+                if consume is not None:
+                    consume(w, rank, k * page_blocks, comp[mine[k]: mine[k + 1]],
+                            lens_all[rank][k * page_blocks: (k + 1) * page_blocks])
+            stats["gathered_bytes"] += mine[-1]
+            live = {}         # (peer, ring index) -> (work, page, lo, hi)
+
+            def finish(key):
+                q, k, lo, hi = live.pop(key)
+                q.wait()      # GPU: the side stream waits for the receive (no host wait)
+                if consume is not None:
+                    consume(w, key[0], k * page_blocks, slots[key][: hi - lo],
+                            lens_all[key[0]][k * page_blocks: (k + 1) * page_blocks])
+
+            npages = max((len(host_bounds[r]) - 1 for r in range(world) if r != rank), default=0)
+            for k in range(npages):
+                for r in range(world):
+                    if r == rank or k >= len(host_bounds[r]) - 1:
+                        continue
+                    lo, hi = host_bounds[r][k], host_bounds[r][k + 1]
+                    if hi == lo:
+                        continue
+                    key = (r, k % ring)
+                    if key in live:
+                        finish(key)   # its consume is ordered before the next receive into the slot
+                    buf = slots.get(key)
+                    if buf is None or buf.numel() < hi - lo:
+                        slots[key] = buf = torch.empty(max(hi - lo, 1 << 20), dtype=torch.uint8, device=dev)
+                    live[key] = (dist.irecv(buf[: hi - lo], src=_global(r, group), group=group), k, lo, hi)
+                    stats["gathered_bytes"] += hi - lo
+                    stats["pages"] += 1
+            for key in list(live):
+                finish(key)
+
+    def release(w):
+        """Order the current stream after wave w's transfers (its buffers are reused)."""
+        for q in sends.pop(w, []):
+            q.wait()
+        if side is not None:
+            side.before_current()
 
     for w in range(waves):
+        if w >= 2:
+            release(w - 2)
         comp, lens = compress_wave(w)
-        stats["comp_bytes"] += comp.numel()
-        stats["blocks"] += lens.numel()
-        if pending is not None and not overlap:
-            done(*pending)
-            pending = None
-        h = gather_start(comp, lens, root, group, out=bufs[w & 1] if rank == root else None)
-        if pending is not None:
-            done(*pending)
-        pending = (w, h)
+        if side is None:
+            side = _Side(comp.device)
+        ev = side.mark()
         if not overlap:
-            done(*pending)
-            pending = None
+            post(w, comp, lens, ev)
+            release(w)
+            continue
+        if pending is not None:
+            post(*pending)          # wave w - 1, while wave w compresses
+        pending = (w, comp, lens, ev)
     if pending is not None:
-        done(*pending)
+        post(*pending)
+    for w in list(sends):
+        release(w)
+    if side is not None:
+        side.before_current()
     return stats
 
 

@@ -9,6 +9,7 @@ is missing, every entry point raises ``RuntimeError``.
 """
 from __future__ import annotations
 
+import collections
 import ctypes as C
 import os
 import threading
@@ -30,7 +31,7 @@ LINKED_SERIAL = 1        # lz4m_compress_linked_batch modes
 LINKED_SPECULATIVE = 2
 EINVAL = 0x10000
 # decoder selector of lz4m_decompress_batch_sel (include/lz4m.h)
-DECODERS = {"auto": 0, "lane": 1, "coop": 2, "hist": 3, "rows": 4, "direct": 5, "quad": 6}
+DECODERS = {"auto": 0, "hist": 3, "rows": 4, "quad": 6}
 
 _lock = threading.Lock()
 _lib = None
@@ -130,7 +131,7 @@ def launch_decompress(src, src_off, src_len, dst, dst_off, dst_cap, status, n, s
     L = lib()
     sp = stream_ptr(stream)
     if dict_buf is None:
-        work = _workspace(src.device, sp, n, src.numel() if src_bytes is None else src_bytes)
+        work = _workspace(src.device, stream, n, src.numel() if src_bytes is None else src_bytes)
         rc = L.lz4m_decompress_batch_sel(ptr(src), ptr(src_off), ptr(src_len), ptr(dst), ptr(dst_off), ptr(dst_cap),
                                          ptr(status), n, ptr(work), work.numel(), DECODERS[decoder], sp)
     else:
@@ -140,20 +141,28 @@ def launch_decompress(src, src_off, src_len, dst, dst_off, dst_cap, status, n, s
     check(rc, "lz4m_decompress_batch")
 
 
-_WORK = {}
+_WORK: "collections.OrderedDict" = collections.OrderedDict()
+_WORK_STREAMS = 4   # scratch buffers kept (least recently used streams dropped first)
 
 
-def _workspace(dev, sp, n: int = 0, src_bytes: int = 0) -> torch.Tensor:
+def _workspace(dev, stream, n: int = 0, src_bytes: int = 0) -> torch.Tensor:
     """Decoder scratch (lz4m_decompress_workspace_size), one buffer per
     (device, stream), grown on demand: calls on one stream are ordered, so
-    they can share it."""
-    key = (dev, sp)
+    they can share it.  The buffer is allocated on the stream that uses it,
+    so when it is dropped (regrowth, eviction, release_workspaces) the
+    caching allocator hands its memory only to work ordered after that
+    stream's pending launches.  At most _WORK_STREAMS buffers are cached."""
+    s = stream if stream is not None else torch.cuda.current_stream(dev)
+    key = (dev, int(s.cuda_stream))
     need = int(lib().lz4m_decompress_workspace_size(n, src_bytes))
-    w = _WORK.get(key)
+    w = _WORK.pop(key, None)
     if w is None or w.numel() < need:
-        _WORK.pop(key, None)
-        w = torch.empty(need, dtype=torch.uint8, device=dev)
-        _WORK[key] = w
+        w = None
+        with torch.cuda.stream(s):
+            w = torch.empty(need, dtype=torch.uint8, device=dev)
+    _WORK[key] = w
+    while len(_WORK) > _WORK_STREAMS:
+        _WORK.popitem(last=False)
     return w
 
 

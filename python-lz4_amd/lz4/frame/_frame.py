@@ -553,6 +553,10 @@ def _decode_linked(d_frame, c_off, c_len, raw_mask, out, status, maxb):
     dlen = torch.clamp(slot_off, max=65536)
     dict_off = slot_off - dlen
     dlen = dlen.to(torch.int32)
+    # both buffers start zeroed: the decoder leaves a slot's bytes past the
+    # block's decoded length untouched, so a short last block (or a failing
+    # one) must see equal bytes there in both or the fixed point never shows
+    out[:span].zero_()
     bufs = [out, torch.zeros_like(out)]
     sts = [torch.empty(nb, dtype=torch.int32, device=dev), torch.empty(nb, dtype=torch.int32, device=dev)]
     sel_r = torch.nonzero(raw_mask).flatten()

@@ -76,6 +76,12 @@ def test_argument_validation_without_gpu():
                                           N.LINKED_SPECULATIVE, None, 0, None) == N.EINVAL
     assert lib.lz4m_compress_linked_workspace_size(4) >= 4 * 2 * 16384
     assert lib.lz4m_xxh32_batch(None, None, None, 0, None, -1, None) == N.EINVAL
+    # retired decoder ids (1 lane, 2 coop, 5 direct) and unknown ids are rejected before any launch
+    for dec in (1, 2, 5, 7, -1):
+        assert lib.lz4m_decompress_batch_sel(None, None, None, None, None, None, None, 0, None, 0, dec,
+                                             None) == N.EINVAL
+    for dec in N.DECODERS.values():
+        assert lib.lz4m_decompress_batch_sel(None, None, None, None, None, None, None, 0, None, 0, dec, None) == 0
     assert lib.lz4m_xxh32_long(None, -1, 0, None, None) == N.EINVAL
     assert lib.lz4m_frame_scan(None, -1, 0, 0, 0, 65536, 1, None, None, None, None, None) == N.EINVAL
     assert lib.lz4m_frame_scan(None, 16, 0, 0, 0, 65536, 1, None, None, None, None, None) == N.EINVAL

@@ -77,43 +77,57 @@ def test_gather_compressed_gloo(world, counts, root):
 
 def _wave_worker(rank, world, port, waves, q):
     """The config-5 wave driver with a CPU stand-in for the compressor: each
-    wave yields this rank's chunk of seeded variable-length 'blocks'."""
+    wave yields this rank's chunk of seeded variable-length 'blocks', padded
+    past the blocks' end like a compaction buffer."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from lz4._dist import compress_gather_waves
     try:
+        def blocks(r, w):
+            return _shard_blocks(r * 100 + w, 3 + 2 * ((w + r) % 4))
+
         def wave(w):
-            return _shard_blocks(rank * 100 + w, 3 + (w + rank) % 4)
+            data, lens = blocks(rank, w)
+            return torch.cat([data, torch.full((17,), 0xEE, dtype=torch.uint8)]), lens
 
         got = {}
 
-        def consume(w, buf, off, lens):
-            got[w] = (buf.clone(), off.clone(), lens.clone())
+        def consume(w, r, first, buf, lens):
+            got.setdefault((w, r), []).append((first, buf.clone(), lens.clone()))
 
-        for overlap in (True, False):
+        oks = []
+        for overlap, page_blocks, ring in ((True, 2, 2), (False, 3, 1), (True, 4096, 4)):
             got.clear()
-            st = compress_gather_waves(wave, waves, root=0, overlap=overlap, consume=consume)
+            st = compress_gather_waves(wave, waves, root=0, overlap=overlap, consume=consume,
+                                       page_blocks=page_blocks, ring=ring)
+            ok = st["waves"] == waves
             if rank == 0:
-                ok = sorted(got) == list(range(waves))
-                for w in range(waves):
-                    parts = [_shard_blocks(r * 100 + w, 3 + (w + r) % 4) for r in range(world)]
-                    buf, off, lens = got[w]
-                    ok = ok and torch.equal(buf, torch.cat([p[0] for p in parts]))
-                    ok = ok and torch.equal(lens, torch.cat([p[1] for p in parts]))
-                    ok = ok and torch.equal(off[1:], torch.cumsum(lens[:-1].to(torch.int64), 0))
-                ok = ok and st["gathered_bytes"] == sum(int(got[w][0].numel()) for w in range(waves))
-                q.put(("root", bool(ok)))
+                ok = ok and sorted(got) == [(w, r) for w in range(waves) for r in range(world)]
+                total = 0
+                for (w, r), pages in got.items():
+                    data, lens = blocks(r, w)
+                    firsts = [f for f, _, _ in pages]
+                    ok = ok and firsts == list(range(0, lens.numel(), page_blocks))
+                    ok = ok and torch.equal(torch.cat([b for _, b, _ in pages]), data)
+                    ok = ok and torch.equal(torch.cat([x for _, _, x in pages]), lens)
+                    ok = ok and all(int(x.to(torch.int64).sum()) == b.numel() for _, b, x in pages)
+                    total += data.numel()
+                ok = ok and st["gathered_bytes"] == total
             else:
-                q.put(("peer", st["waves"] == waves and not got))
+                ok = ok and not got and st["comp_bytes"] == sum(int(blocks(rank, w)[1].sum()) for w in range(waves))
+            oks.append(bool(ok))
+        q.put(("root" if rank == 0 else "peer", all(oks), oks))
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("world,waves", [(2, 3), (3, 2)])
 def test_wave_driver_gloo(world, waves):
-    """compress -> compact -> gather per wave, gathers overlapped with the next
-    wave (and not), world size 2 and 3 over gloo: the root receives every
-    wave's blocks in rank order with the right index."""
+    """compress -> compact -> paged gather per wave, gathers overlapped with
+    the next wave (and not), world size 2 and 3 over gloo, pages of 2, 3 and
+    4096 blocks through a ring of 2, 1 and 4 receive buffers: the root
+    consumes every rank's blocks of every wave, page by page, with their
+    sizes."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -123,5 +137,5 @@ def test_wave_driver_gloo(world, waves):
     for p in procs:
         p.join(180)
         assert p.exitcode == 0
-    res = [q.get(timeout=10) for _ in range(2 * world)]
-    assert all(ok for _, ok in res), res
+    res = [q.get(timeout=10) for _ in range(world)]
+    assert all(r[1] for r in res), res

@@ -364,6 +364,37 @@ def test_frame_linked_decode_modes(gpu, reference, monkeypatch, mode):
     assert lz4.frame.decompress(f) == a + b + c
 
 
+def test_frame_linked_short_last_block_rounds(gpu, monkeypatch):
+    """A linked frame whose last block is short (size not a multiple of the
+    block size) reaches the speculative fixed point in a few rounds, not
+    nb + 1: the slot bytes past the short block compare equal between the two
+    round buffers.  Also a frame whose middle block is corrupt."""
+    from lz4 import _native as N
+    from lz4 import _synth
+    calls = []
+    real = N.launch_decompress_prefix
+
+    def counting(*a, **k):
+        calls.append(1)
+        return real(*a, **k)
+
+    monkeypatch.setattr(N, "launch_decompress_prefix", counting)
+    data = _synth.blocks(40, "silesia", seed=5).tobytes()[: 40 * 65536 - 12345]
+    f = lz4.frame.compress(data)                 # 64 KiB linked blocks, last one short
+    assert lz4.frame.decompress(f) == data
+    assert 2 <= len(calls) <= 16, len(calls)   # nb + 1 = 41 before the fix
+    # corrupt a middle block's payload: still an error, still few rounds
+    calls.clear()
+    bad = bytearray(f)
+    bad[7 + 4 + 20 * 30000] ^= 0xFF
+    try:
+        out = lz4.frame.decompress(bytes(bad))
+        assert out != data
+    except RuntimeError:
+        pass
+    assert len(calls) <= 16, len(calls)
+
+
 def test_frame_decodes_reference_frames(gpu, golden):
     man, arr = golden
     inputs = {e["name"]: _b(arr, e["key"]) for e in man["inputs"]}

@@ -27,7 +27,7 @@ def _pack(blocks):
 
 # every decoder (include/lz4m.h lz4m_decompress_batch_sel) must give the
 # reference's bytes and statuses; "auto" is the size-based default
-DECODERS = ["auto", "rows", "quad", "lane", "hist"]
+DECODERS = ["auto", "rows", "quad", "hist"]
 
 
 def gpu_decompress(blocks, caps, dev, decoder="auto"):
@@ -82,7 +82,7 @@ def corpus():
     return blocks, ragged
 
 
-@pytest.mark.parametrize("decoder", DECODERS + ["coop", "direct"])
+@pytest.mark.parametrize("decoder", DECODERS)
 def test_decompress_matches_oracle(gpu, oracle, corpus, decoder):
     blocks, ragged = corpus
     src = blocks + ragged + [bytes(65536), bytes([7]) * 65536, b"ab" * 32768]
@@ -146,7 +146,7 @@ def malformed_cases(oracle, blocks, count=3000, seed=1234):
     return cases, caps
 
 
-@pytest.mark.parametrize("decoder", DECODERS + ["coop", "direct"])
+@pytest.mark.parametrize("decoder", DECODERS)
 def test_decompress_malformed_matches_oracle(gpu, oracle, corpus, decoder):
     blocks, _ = corpus
     cases, caps = malformed_cases(oracle, blocks)
@@ -315,7 +315,7 @@ def _offset0_block(lit, ml):
     return seq + bytes([5 << 4]) + b"tail!"
 
 
-@pytest.mark.parametrize("decoder", ["auto", "quad", "lane"])
+@pytest.mark.parametrize("decoder", ["auto", "quad", "hist"])
 def test_decompress_large_batch_edges(gpu, oracle, corpus, decoder):
     """A batch above the small-batch switch-over (32 768 blocks), so the
     default dispatch runs the large-batch decoder, with every edge case of the

@@ -1,6 +1,6 @@
 """Dev probe: decode time per decoder (LZ4M decoders via lz4m_decompress_batch_sel)
 on NBLK x 64 KiB blocks of each KIND, verified against the input.
-env: NBLK (default 262144), KINDS (silesia), DECS (rows,lane,hist), REPS (3)."""
+env: NBLK (default 262144), KINDS (silesia), DECS (rows,hist), REPS (3)."""
 import json
 import os
 import sys
@@ -33,7 +33,7 @@ for kind in os.environ.get("KINDS", "silesia").split(","):
     doff = torch.arange(n, dtype=torch.int64, device=dev) * 65536
     dcap = torch.full((n,), 65536, dtype=torch.int32, device=dev)
     st = torch.empty(n, dtype=torch.int32, device=dev)
-    for dec in os.environ.get("DECS", "rows,lane,hist").split(","):
+    for dec in os.environ.get("DECS", "rows,hist").split(","):
         dst.zero_()
         t0 = time.time()
         N.launch_decompress(comp, coff, olen, dst, doff, dcap, st, n, decoder=dec)
