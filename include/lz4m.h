@@ -77,6 +77,20 @@ int lz4m_compress_dict_batch(const uint8_t* d_src, const int64_t* d_src_off, con
                              lz4m_stream_t stream);
 
 /*
+ * The same call when the caller's dictionary memory ends exactly where the
+ * source begins (lz4.block.compress(src, dict=D) with D and src slices of one
+ * buffer, D >= 8 bytes): LZ4_compress_fast_continue then sees
+ * dictEnd == source and compresses in prefix mode (lz4.c:1671-1676,
+ * withPrefix64k) instead of usingExtDict: backward catch-up of every match
+ * may reach into the dictionary (lowLimit = source - dictSize, lz4.c:967).
+ * Same layout and arguments as lz4m_compress_dict_batch.
+ */
+int lz4m_compress_prefix_batch(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len,
+                               const int32_t* d_dict_len, uint8_t* d_dst, const int64_t* d_dst_off,
+                               const int32_t* d_dst_cap, int32_t* d_out_len, int64_t n, int acceleration,
+                               lz4m_stream_t stream);
+
+/*
  * Batched linked-block compression: the blocks of one stream are compressed
  * as consecutive LZ4_compress_fast_continue calls on one LZ4_stream_t that
  * was freshly initialised (LZ4F_compressBlock_continue, lz4frame.c:865-871;

@@ -343,11 +343,26 @@ last_literals:
     return (int)(op - dst);
 }
 
+int orc_compress_dict_mode(const uint8_t* win, int64_t d_len, int n, uint8_t* dst, int cap, int accel, int prefix);
+
 /* lz4.block.compress(source, dict=D) for a non-HC mode (_block.c:93-107):
  * LZ4_resetStream, LZ4_loadDict (lz4.c:1541-1581: last 64 KiB of D, every
  * third position hashed, indexes ending at 64 KiB), LZ4_compress_fast_continue.
  * `win` holds the last min(d_len, 65536) bytes of D followed by the source. */
 int orc_compress_dict(const uint8_t* win, int64_t d_len, int n, uint8_t* dst, int cap, int accel)
+{
+    return orc_compress_dict_mode(win, d_len, n, dst, cap, accel, 0);
+}
+
+/* The same call when D's memory ends exactly where the source begins
+ * (prefix = 1): LZ4_compress_fast_continue sees dictEnd == source and takes
+ * prefix mode (lz4.c:1671-1676, withPrefix64k) instead of usingExtDict, so
+ * backward catch-up of EVERY match may reach back to the dictionary's first
+ * byte (lowLimit = source - dictSize, lz4.c:967) -- with extDict a match
+ * inside the source stops at the source start (lz4.c:1052-1053).  Valid-area
+ * (dictSmall: prefixIdxLimit = startIndex - dictSize, lz4.c:937/1061) and
+ * distance rules are the same in both modes. */
+int orc_compress_dict_mode(const uint8_t* win, int64_t d_len, int n, uint8_t* dst, int cap, int accel, int prefix)
 {
     uint32_t table[4096];
     memset(table, 0, sizeof(table));
@@ -359,7 +374,7 @@ int orc_compress_dict(const uint8_t* win, int64_t d_len, int n, uint8_t* dst, in
         int64_t p;
         for (p = 0; p <= dt - 8; p += 3)                           /* lz4.c:1575-1578 */
             table[orc_hash(win + p, ORC_TABLE_U32_HASH5)] = ibase + (uint32_t)p;
-        return orc_compress_window(win, dt, n, dst, cap, accel, table, ibase, ibase, dt, 0);
+        return orc_compress_window(win, dt, n, dst, cap, accel, table, ibase, ibase, prefix ? 0 : dt, 0);
     }
 }
 

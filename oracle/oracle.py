@@ -70,6 +70,8 @@ class Oracle:
         lib.orc_decompress_batch.argtypes = [vp, vp, vp, vp, vp, vp, vp, i64]
         lib.orc_compress_dict.argtypes = [vp, i64, i32, vp, i32, i32]
         lib.orc_compress_dict.restype = i32
+        lib.orc_compress_dict_mode.argtypes = [vp, i64, i32, vp, i32, i32, i32]
+        lib.orc_compress_dict_mode.restype = i32
         lib.orc_compress_linked.argtypes = [vp, i64, i32, i32, vp, i64, vp]
         lib.orc_compress_linked.restype = i32
         self.lib = lib
@@ -85,15 +87,16 @@ class Oracle:
         r = self.lib.orc_compress(sp, n, dst.ctypes.data_as(C.c_void_p), cap, variant, accel)
         return None if r <= 0 else dst[:r].tobytes()
 
-    def compress_dict(self, data, dict_, accel: int = 1) -> bytes | None:
-        """lz4.block.compress(data, dict=dict_, store_size=False) (_block.c:93-107)."""
+    def compress_dict(self, data, dict_, accel: int = 1, prefix: bool = False) -> bytes | None:
+        """lz4.block.compress(data, dict=dict_, store_size=False) (_block.c:93-107).
+        ``prefix``: dict_'s memory ends where data begins (prefix mode, lz4.c:1671)."""
         d = bytes(dict_)
         tail = d[-65536:] if len(d) >= 8 else b""
         win, wp = _buf(tail + bytes(data))
         n = win.size - len(tail)
         cap = compress_bound(n)
         dst = np.zeros(max(cap, 1), dtype=np.uint8)
-        r = self.lib.orc_compress_dict(wp, len(d), n, dst.ctypes.data_as(C.c_void_p), cap, accel)
+        r = self.lib.orc_compress_dict_mode(wp, len(d), n, dst.ctypes.data_as(C.c_void_p), cap, accel, int(prefix))
         return None if r <= 0 else dst[:r].tobytes()
 
     def compress_linked(self, data, block_size: int, accel: int = 1) -> list:
@@ -195,6 +198,22 @@ class Reference:
         self.lib.LZ4_resetStream(state)
         self.lib.LZ4_loadDict(state, d.ctypes.data_as(C.c_void_p), d.size - 1)
         r = self.lib.LZ4_compress_fast_continue(state, sp, dst.ctypes.data_as(C.c_void_p), src.size, cap, accel)
+        return dst[:r].tobytes()
+
+    def compress_dict_prefix(self, data, dict_, accel: int = 1) -> bytes:
+        """lz4.block.compress(data, dict=dict_) when dict_'s memory ends exactly
+        where data begins (memoryview slices of one buffer): the reference's
+        LZ4_compress_fast_continue then sees dictEnd == source (lz4.c:1671)."""
+        buf = np.frombuffer(bytes(dict_) + bytes(data) + b"\0", dtype=np.uint8)
+        base = buf.ctypes.data
+        n = len(data)
+        cap = compress_bound(n)
+        dst = np.zeros(max(cap, 1), dtype=np.uint8)
+        state = C.create_string_buffer(int(self.lib.LZ4_sizeofState()))
+        self.lib.LZ4_resetStream(state)
+        self.lib.LZ4_loadDict(state, C.c_void_p(base), len(dict_))
+        r = self.lib.LZ4_compress_fast_continue(state, C.c_void_p(base + len(dict_)), dst.ctypes.data_as(C.c_void_p),
+                                                n, cap, accel)
         return dst[:r].tobytes()
 
     def decompress(self, data, cap: int, dict_=None) -> tuple[int, bytes]:

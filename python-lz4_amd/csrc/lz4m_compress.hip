@@ -705,7 +705,8 @@ __global__ __launch_bounds__(64) void compress_dict_kernel(const uint8_t* __rest
                                                            const int32_t* __restrict__ dict_len, uint8_t* dst,
                                                            const int64_t* __restrict__ dst_off,
                                                            const int32_t* __restrict__ dst_cap,
-                                                           int32_t* __restrict__ out_len, int64_t n, int accel) {
+                                                           int32_t* __restrict__ out_len, int64_t n, int accel,
+                                                           int prefix) {
     __shared__ __attribute__((aligned(16))) uint16_t tab[8192];
     RING_DECL
     uint32_t* t32 = reinterpret_cast<uint32_t*>(tab);
@@ -730,8 +731,12 @@ __global__ __launch_bounds__(64) void compress_dict_kernel(const uint8_t* __rest
                 atomicMax(&t32[TabU32::hash(w + p)], ibase + (uint32_t)p);
             __builtin_amdgcn_s_waitcnt(0xc07f);
         }
+        // catch-up floor of matches inside the block: the block start
+        // (usingExtDict, lz4.c:1052-1053) or, in prefix mode, the dictionary
+        // start like every other match (lz4.c:967)
+        const int32_t low_src = prefix ? 0 : hist;
         const int32_t r = compress_block_w<LZ4M_TABLE_U32_HASH5>(w, hist, (int32_t)len, dst + dst_off[b], dst_cap[b],
-                                                                 accel, tab, ring, lane, ibase, low_idx, hist, 0);
+                                                                 accel, tab, ring, lane, ibase, low_idx, low_src, 0);
         if (lane == 0) out_len[b] = (int32_t)r;
     }
 }
@@ -925,18 +930,34 @@ extern "C" int lz4m_compress_batch(const uint8_t* d_src, const int64_t* d_src_of
     return (int)hipGetLastError();
 }
 
-extern "C" int lz4m_compress_dict_batch(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len,
-                                        const int32_t* d_dict_len, uint8_t* d_dst, const int64_t* d_dst_off,
-                                        const int32_t* d_dst_cap, int32_t* d_out_len, int64_t n, int acceleration,
-                                        lz4m_stream_t stream) {
+static int compress_dict_launch(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len,
+                                const int32_t* d_dict_len, uint8_t* d_dst, const int64_t* d_dst_off,
+                                const int32_t* d_dst_cap, int32_t* d_out_len, int64_t n, int acceleration,
+                                int prefix, lz4m_stream_t stream) {
     if (n < 0) return LZ4M_EINVAL;
     if (n == 0) return 0;
     if (acceleration < 1) acceleration = 1;
     if (acceleration > 65537) acceleration = 65537;
     const uint32_t grid = (uint32_t)(n < (1ll << 30) ? n : (1ll << 30));
     hipLaunchKernelGGL(compress_dict_kernel, dim3(grid), dim3(64), 0, (hipStream_t)stream, d_src, d_src_off,
-                       d_src_len, d_dict_len, d_dst, d_dst_off, d_dst_cap, d_out_len, n, acceleration);
+                       d_src_len, d_dict_len, d_dst, d_dst_off, d_dst_cap, d_out_len, n, acceleration, prefix);
     return (int)hipGetLastError();
+}
+
+extern "C" int lz4m_compress_dict_batch(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len,
+                                        const int32_t* d_dict_len, uint8_t* d_dst, const int64_t* d_dst_off,
+                                        const int32_t* d_dst_cap, int32_t* d_out_len, int64_t n, int acceleration,
+                                        lz4m_stream_t stream) {
+    return compress_dict_launch(d_src, d_src_off, d_src_len, d_dict_len, d_dst, d_dst_off, d_dst_cap, d_out_len, n,
+                                acceleration, 0, stream);
+}
+
+extern "C" int lz4m_compress_prefix_batch(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len,
+                                          const int32_t* d_dict_len, uint8_t* d_dst, const int64_t* d_dst_off,
+                                          const int32_t* d_dst_cap, int32_t* d_out_len, int64_t n, int acceleration,
+                                          lz4m_stream_t stream) {
+    return compress_dict_launch(d_src, d_src_off, d_src_len, d_dict_len, d_dst, d_dst_off, d_dst_cap, d_out_len, n,
+                                acceleration, 1, stream);
 }
 
 extern "C" int lz4m_compress_prof(unsigned long long* out, int reset) {

@@ -53,6 +53,7 @@ def _declare(lib) -> None:
         "lz4m_decompress_chain": ([vp, vp, vp, vp, vp, vp, i64, i32, vp], i32),
         "lz4m_compress_batch": ([vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, vp], i32),
         "lz4m_compress_dict_batch": ([vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, vp], i32),
+        "lz4m_compress_prefix_batch": ([vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, vp], i32),
         "lz4m_compress_linked_workspace_size": ([i64], C.c_size_t),
         "lz4m_compress_linked_passes": ([], i32),
         "lz4m_compress_linked_batch": ([vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, vp, C.c_size_t, vp], i32),
@@ -197,11 +198,14 @@ def launch_compress(src, src_off, src_len, dst, dst_off, dst_cap, out_len, n, ta
 
 
 def launch_compress_dict(src, src_off, src_len, dict_len, dst, dst_off, dst_cap, out_len, n, accel,
-                         stream=None) -> None:
-    """lz4.block.compress(dict=) per block; the dictionary tail precedes each block in ``src``."""
-    rc = lib().lz4m_compress_dict_batch(ptr(src), ptr(src_off), ptr(src_len), ptr(dict_len), ptr(dst), ptr(dst_off),
-                                        ptr(dst_cap), ptr(out_len), n, accel, stream_ptr(stream))
-    check(rc, "lz4m_compress_dict_batch")
+                         stream=None, prefix: bool = False) -> None:
+    """lz4.block.compress(dict=) per block; the dictionary tail precedes each block in ``src``.
+    ``prefix``: the caller's dictionary ends where the source begins (prefix mode,
+    lz4m_compress_prefix_batch)."""
+    name = "lz4m_compress_prefix_batch" if prefix else "lz4m_compress_dict_batch"
+    rc = getattr(lib(), name)(ptr(src), ptr(src_off), ptr(src_len), ptr(dict_len), ptr(dst), ptr(dst_off),
+                              ptr(dst_cap), ptr(out_len), n, accel, stream_ptr(stream))
+    check(rc, name)
 
 
 def launch_compress_linked(src, src_off, src_len, link, dst, dst_off, dst_cap, out_len, n, accel,

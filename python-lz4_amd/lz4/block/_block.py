@@ -122,8 +122,12 @@ def compress(source, mode="default", store_size=True, acceleration=1, compressio
             out[:4] = n.to_bytes(4, "little")
         del out[hdr + r:]
         return out if return_bytearray else bytes(out)
+    # dictionary memory that ends where the source begins: the reference's
+    # LZ4_compress_fast_continue sees dictEnd == source and takes prefix mode
+    # (lz4.c:1671-1676; LZ4_loadDict keeps no dictionary below 8 bytes)
+    prefix = d.nbytes >= 8 and src.nbytes > 0 and _addr(d) + d.nbytes == _addr(src)
     out = compress_many([src], accel=accel, store_size=bool(store_size), as_bytearray=bool(return_bytearray),
-                        dict=d)[0]
+                        dict=d, dict_prefix=prefix)[0]
     if out is None:
         raise LZ4BlockError("Compression failed")
     return out
@@ -265,12 +269,14 @@ def _stage_out(lay: _Layout, h: torch.Tensor, d: torch.Tensor, n: int):
 
 
 def compress_many(blocks, accel: int = 1, store_size: bool = True, as_bytearray: bool = False,
-                  table: int = N.TABLE_U32_HASH5, dict=None):
+                  table: int = N.TABLE_U32_HASH5, dict=None, dict_prefix: bool = False):
     """Compress a sequence of host buffers as independent blocks in one
     launch.  Returns a list of bytes (None for a block that failed, i.e.
     input larger than LZ4_MAX_INPUT_SIZE).  ``dict`` (a buffer, possibly
     empty): every block is compressed as lz4.block.compress(dict=dict) does;
-    the dictionary's last 64 KiB are staged in front of each block."""
+    the dictionary's last 64 KiB are staged in front of each block.
+    ``dict_prefix``: compress as the reference does when the dictionary's
+    memory ends where each source begins (prefix mode, lz4.c:1671)."""
     views = [_buffer(b) for b in blocks]
     dev = N.device()
     n = len(views)
@@ -295,7 +301,8 @@ def compress_many(blocks, accel: int = 1, store_size: bool = True, as_bytearray:
         N.launch_compress(d_src, src_off, src_len, d_dst, dst_off, dst_cap, out_len, n, table, accel)
     else:
         dict_len = torch.full((n,), dv.nbytes, dtype=torch.int32, device=dev)
-        N.launch_compress_dict(d_src, src_off, src_len, dict_len, d_dst, dst_off, dst_cap, out_len, n, accel)
+        N.launch_compress_dict(d_src, src_off, src_len, dict_len, d_dst, dst_off, dst_cap, out_len, n, accel,
+                               prefix=dict_prefix and dv.nbytes >= 8)
     olen, host = _stage_out(lay, h, d, n)
     res = []
     for i in range(n):

@@ -12,6 +12,8 @@ records inputs and the reference's outputs:
     linked blocks);
   * lz4.block.compress(dict=) outputs (LZ4_resetStream + LZ4_loadDict +
     LZ4_compress_fast_continue, _block.c:93-107) for dictionaries of 0..100000 B;
+  * the same with the dictionary's memory ending where the source begins
+    (prefix mode, lz4.c:1671-1676), as memoryview slices of one buffer give;
   * the reference tests' own data file tests/block/numpy_byte_array.bin and
     the known-answer vectors of tests/block/test_block_1.py:128-149.
 Vectors are data only; nothing of the reference's source is stored.
@@ -143,6 +145,26 @@ def main():
         c = ref.compress_dict(data, dd, acc)
         man["dict_compress"].append({"input": name, "dict": add(f"dict_{i}", dd), "accel": acc,
                                      "key": add(f"cdict_{i}", c)})
+
+    # lz4.block.compress(source, dict=D) with D's memory ending where the
+    # source begins (slices of one buffer): prefix mode (lz4.c:1671-1676)
+    man["dict_prefix_compress"] = []
+    blob = _synth.blocks(3, "silesia", seed=79).tobytes()
+    pcases = [(65536, 8, 4000, 1), (65536, 65536, 65536, 1), (1000, 9, 13, 1), (100, 100, 5, 1)]
+    prng = random.Random(1671)
+    while len(pcases) < 16:   # plus cases whose prefix-mode bytes differ from extDict's
+        cut = prng.randrange(8, len(blob) - 70000)
+        dl = min(prng.choice([8, 12, 50, 300, 5000, 65536, 70000]), cut)
+        n, acc = prng.choice([700, 4000, 12000, 65536]), prng.choice([1, 1, 2, 8])
+        dd, data = blob[cut - dl:cut], blob[cut:cut + n]
+        if ref.compress_dict_prefix(data, dd, acc) != ref.compress_dict(data, dd, acc):
+            pcases.append((cut, dl, n, acc))
+    for i, (cut, dl, n, acc) in enumerate(pcases):
+        dd, data = blob[cut - dl:cut], blob[cut:cut + n]
+        c = ref.compress_dict_prefix(data, dd, acc)
+        man["dict_prefix_compress"].append({"input": add(f"pdict_src_{i}", data), "dict": add(f"pdict_{i}", dd),
+                                            "accel": acc, "key": add(f"cpdict_{i}", c),
+                                            "extdict_differs": c != ref.compress_dict(data, dd, acc)})
 
     np.savez_compressed(os.path.join(HERE, "golden.npz"), **arrays)
     with open(os.path.join(HERE, "manifest.json"), "w") as f:

@@ -164,6 +164,24 @@ def test_block_dict_compress_golden(gpu, golden):
         assert lz4.block.decompress(got, uncompressed_size=len(data), dict=d) == data
 
 
+def test_block_dict_prefix_compress_golden(gpu, golden):
+    """lz4.block.compress(src, dict=D) with D and src slices of ONE buffer
+    (D's memory ends where src begins): the reference compresses in prefix
+    mode (lz4.c:1671-1676); byte-identical to its golden outputs, and the
+    same bytes staged as separate objects still give the extDict parse."""
+    man, arr = golden
+    for e in man["dict_prefix_compress"]:
+        data, d = _b(arr, e["input"]), _b(arr, e["dict"])
+        mv = memoryview(d + data)
+        mode = ("default", 1) if e["accel"] == 1 else ("fast", e["accel"])
+        got = lz4.block.compress(mv[len(d):], mode=mode[0], acceleration=mode[1], store_size=False,
+                                 dict=mv[:len(d)])
+        assert got == _b(arr, e["key"]), e
+        assert lz4.block.decompress(got, uncompressed_size=len(data), dict=d) == data
+        sep = lz4.block.compress(data, mode=mode[0], acceleration=mode[1], store_size=False, dict=d)
+        assert (sep != got) == e["extdict_differs"], e
+
+
 def test_block_dict_compress_vs_oracle(gpu, oracle):
     """Batched dict= compression over dictionary lengths around every
     LZ4_loadDict boundary, against the CPU restatement."""

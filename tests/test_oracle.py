@@ -170,6 +170,36 @@ def test_dict_compress_golden(oracle, golden):
         assert got == _b(arr, e["key"]), e
 
 
+def test_dict_prefix_compress_golden(oracle, golden):
+    """Dictionary memory ending where the source begins: the reference takes
+    prefix mode (lz4.c:1671-1676), and the restatement reproduces it; at least
+    a dozen of the golden cases differ from the extDict bytes."""
+    man, arr = golden
+    cases = man["dict_prefix_compress"]
+    assert sum(e["extdict_differs"] for e in cases) >= 10
+    for e in cases:
+        data, d = _b(arr, e["input"]), _b(arr, e["dict"])
+        assert oracle.compress_dict(data, d, e["accel"], prefix=True) == _b(arr, e["key"]), e
+        assert (oracle.compress_dict(data, d, e["accel"]) != _b(arr, e["key"])) == e["extdict_differs"], e
+
+
+def test_dict_prefix_vs_reference(oracle, reference):
+    """Differential against the compiled reference: prefix-mode dict= over
+    random cuts of one buffer (dictionary 8 B .. > 64 KiB)."""
+    from lz4 import _synth
+    rng = random.Random(1671)
+    for kind in ("text", "records", "runs", "silesia"):
+        blob = _synth.blocks(3, kind, seed=5).tobytes()
+        for _ in range(25):
+            cut = rng.randrange(8, len(blob) - 8)
+            dl = min(rng.choice([8, 12, 50, 300, 5000, 65536, 70000]), cut)
+            n = min(rng.choice([1, 13, 700, 4000, 65536]), len(blob) - cut)
+            d, s = blob[cut - dl:cut], blob[cut:cut + n]
+            acc = rng.choice([1, 2, 9])
+            assert oracle.compress_dict(s, d, acc, prefix=True) == reference.compress_dict_prefix(s, d, acc), \
+                (kind, cut, dl, n, acc)
+
+
 def test_dict_and_linked_vs_reference(oracle, reference):
     """Differential: dictionary lengths around every LZ4_loadDict boundary
     (< 8, 64 KiB, > 64 KiB) and linked frames of every block size."""
