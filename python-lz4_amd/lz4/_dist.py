@@ -195,8 +195,11 @@ def compress_gather_waves(compress_wave, waves: int, root: int = 0, group=None, 
     isend; the root receives them into a ring of `ring` page buffers per peer
     and consumes its own shard in place.  Returns byte counts for rates.
     """
-    rank = dist.get_rank(group)
-    world = dist.get_world_size(group)
+    # one process and no process group (bench.py at N = 1): rank 0 of 1,
+    # nothing to exchange
+    grouped = dist.is_available() and dist.is_initialized()
+    rank = dist.get_rank(group) if grouped else 0
+    world = dist.get_world_size(group) if grouped else 1
     stats = {"waves": waves, "comp_bytes": 0, "gathered_bytes": 0, "blocks": 0, "pages": 0, "host_waits": 0}
     side = None
     sends = {}            # wave -> outstanding send works (buffers of that wave in use)
@@ -208,15 +211,18 @@ def compress_gather_waves(compress_wave, waves: int, root: int = 0, group=None, 
         side.wait(ev)                 # wave w's compression, not the next wave's
         with side.ctx():
             meta = torch.tensor([lens.numel()], dtype=torch.int64, device=dev)
-            metas = [torch.empty_like(meta) for _ in range(world)]
-            dist.all_gather(metas, meta, group=group)
-            counts = [int(x) for x in torch.cat(metas).cpu()]          # host wait (1)
-            mx = max(counts)
-            padded = torch.zeros(mx, dtype=torch.int32, device=dev)
-            padded[: lens.numel()] = lens
-            lens_all = [torch.empty(mx, dtype=torch.int32, device=dev) for _ in range(world)]
-            dist.all_gather(lens_all, padded, group=group)
-            lens_all = [lens_all[r][: counts[r]] for r in range(world)]
+            if world > 1:
+                metas = [torch.empty_like(meta) for _ in range(world)]
+                dist.all_gather(metas, meta, group=group)
+                counts = [int(x) for x in torch.cat(metas).cpu()]          # host wait (1)
+                mx = max(counts)
+                padded = torch.zeros(mx, dtype=torch.int32, device=dev)
+                padded[: lens.numel()] = lens
+                lens_all = [torch.empty(mx, dtype=torch.int32, device=dev) for _ in range(world)]
+                dist.all_gather(lens_all, padded, group=group)
+                lens_all = [lens_all[r][: counts[r]] for r in range(world)]
+            else:
+                lens_all = [lens]
             need = range(world) if rank == root else [rank]
             bounds = {r: _page_bounds(lens_all[r], page_blocks) for r in need}
             hb = torch.cat([bounds[r] for r in need]).cpu().tolist()    # host wait (2), same sync point

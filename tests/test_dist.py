@@ -139,3 +139,33 @@ def test_wave_driver_gloo(world, waves):
         assert p.exitcode == 0
     res = [q.get(timeout=10) for _ in range(world)]
     assert all(r[1] for r in res), res
+
+
+def test_wave_driver_without_process_group():
+    """bench.py at N = 1 starts no process group: the wave driver then runs as
+    rank 0 of 1 (no exchange) and the root consumes its own pages."""
+    from lz4._dist import compress_gather_waves
+    assert not dist.is_initialized()
+    waves, page_blocks = 3, 2
+
+    def wave(w):
+        data, lens = _shard_blocks(w, 5)
+        return torch.cat([data, torch.full((9,), 0xEE, dtype=torch.uint8)]), lens
+
+    got = {}
+
+    def consume(w, r, first, buf, lens):
+        got.setdefault(w, []).append((r, first, buf.clone(), lens.clone()))
+
+    for overlap in (True, False):
+        got.clear()
+        st = compress_gather_waves(wave, waves, root=0, overlap=overlap, consume=consume, page_blocks=page_blocks)
+        assert st["waves"] == waves and st["host_waits"] == 2 * waves
+        for w in range(waves):
+            data, lens = _shard_blocks(w, 5)
+            pages = got[w]
+            assert [p[1] for p in pages] == list(range(0, lens.numel(), page_blocks))
+            assert all(p[0] == 0 for p in pages)
+            assert torch.equal(torch.cat([p[2] for p in pages]), data)
+            assert torch.equal(torch.cat([p[3] for p in pages]), lens)
+        assert st["gathered_bytes"] == st["comp_bytes"] == sum(int(_shard_blocks(w, 5)[1].sum()) for w in range(waves))
