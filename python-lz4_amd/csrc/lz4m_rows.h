@@ -18,11 +18,12 @@ struct RowMeta {
 };
 static_assert(sizeof(RowMeta) == 32, "RowMeta layout");
 
-// scratch layout: 64 bytes of counters, 1 KiB of dummy store targets (the
-// quad executor's unconditional stores of lanes with nothing to store), one
-// RowMeta per block, then the length bytes
+// scratch layout: 64 bytes of counters, 256 KiB of dummy targets (the
+// unconditional loads / stores of lanes with nothing to load or store: 1 KiB
+// per wave slot, blockIdx % 256), one RowMeta per block, then the length bytes
 constexpr size_t kRowsDummy = 64;
-constexpr size_t kRowsMeta = 64 + 1024;
+constexpr size_t kRowsDummySlots = 256;
+constexpr size_t kRowsMeta = kRowsDummy + kRowsDummySlots * 1024;
 
 }  // namespace lz4m
 

@@ -51,6 +51,9 @@ __device__ unsigned long long g_rows_prof[32];
 #define RP_FLUSH(a, b) do {} while (0)
 #endif
 
+// s_waitcnt vmcnt(0) (expcnt and lgkmcnt left at their maximum)
+__device__ __forceinline__ void wait_vm0() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
 // ------------------------------------------------------------- row helpers
 // A row = 16 consecutive lanes; DPP row_shr stays inside a row and
 // row_newbcast:n (gfx90a+) broadcasts lane n of each row to the whole row.
@@ -197,6 +200,14 @@ __device__ __forceinline__ uint32_t dword_at(u32x4 w, uint32_t k) {
     return __builtin_amdgcn_alignbyte(hi, lo, k & 3);
 }
 
+// the 4 bytes at k (0..28) of the 32-byte window a|b
+__device__ __forceinline__ uint32_t dword32(u32x4 a, u32x4 b, uint32_t k) {
+    const uint32_t q = k >> 2;
+    const uint32_t lo = q == 0 ? a.x : q == 1 ? a.y : q == 2 ? a.z : q == 3 ? a.w : q == 4 ? b.x : q == 5 ? b.y : q == 6 ? b.z : b.w;
+    const uint32_t hi = q == 0 ? a.y : q == 1 ? a.z : q == 2 ? a.w : q == 3 ? b.x : q == 4 ? b.y : q == 5 ? b.z : q == 6 ? b.w : 0u;
+    return __builtin_amdgcn_alignbyte(hi, lo, k & 3);
+}
+
 // ------------------------------------------------------------ 1. the parse
 // One lane per block.  The compressed block is read through a 128-byte LDS
 // ring per lane holding stream bytes [wb, wb + 128) (wb a multiple of 64; a
@@ -222,6 +233,9 @@ static_assert(kPStage == 32 || kPStage == 64, "length ring: 32 or 64 entries");
 #define LZ4M_PARSE_WG 64
 #endif
 constexpr int kPWG = LZ4M_PARSE_WG;     // parse workgroup (LDS is allocated per workgroup)
+#ifndef LZ4M_PARSE_PAIR
+#define LZ4M_PARSE_PAIR 1               // the fast loop takes two sequences per step when it can
+#endif
 #ifndef LZ4M_PARSE_MIN_ACTIVE
 #define LZ4M_PARSE_MIN_ACTIVE 40        // run the general step once fewer lanes than this can go on
 #endif
@@ -424,6 +438,9 @@ __global__ __launch_bounds__(kPWG) void rows_parse_kernel(const uint8_t* __restr
                 // straight-line: no short-circuit tests
                 const bool inw = ip + 16 <= wb + kPW;
                 const u32x4 w = lds_ld16(W + (ip & (kPW - 1)));
+#if LZ4M_PARSE_PAIR
+                const u32x4 w2 = lds_ld16(W + ((ip + 16) & (kPW - 1)));   // the next 16 ring bytes
+#endif
                 const int32_t tok = (int32_t)(w.x & 0xFFu), lit = tok >> 4, mlc = tok & 15;
                 const bool mlx = mlc == 15;
                 const uint32_t dw = dword_at(w, (uint32_t)(1 + lit));   // offset, then the match-length byte
@@ -437,9 +454,37 @@ __global__ __launch_bounds__(kPWG) void rows_parse_kernel(const uint8_t* __restr
                 // slot k is free (one slot of the ring always is): written even
                 // when the sequence is not taken, then overwritten
                 stg[k & (kPStage - 1)] = (uint8_t)adv;
+#if LZ4M_PARSE_PAIR
+                // the sequence after it, from the same 32 ring bytes: it
+                // starts at byte adv (<= 16 for a taken sequence) of w|w2
+                const int32_t ip2 = ip + adv, op2 = op + lit + ml;
+                const uint32_t a2 = (uint32_t)adv & 31u;
+                const uint32_t t2 = dword32(w, w2, a2 > 28u ? 28u : a2) >> (8u * (a2 > 28u ? a2 - 28u : 0u));
+                const int32_t tok2 = (int32_t)(t2 & 0xFFu), lit2 = tok2 >> 4, mlc2 = tok2 & 15;
+                const bool mlx2 = mlc2 == 15;
+                const uint32_t p2 = a2 + 1u + (uint32_t)lit2;   // offset, then the match-length byte
+                const uint32_t dw2 = dword32(w, w2, p2 > 28u ? 28u : p2) >> (8u * (p2 > 28u ? p2 - 28u : 0u));
+                const int32_t off2 = (int32_t)(dw2 & 0xFFFFu);
+                const int32_t ext2 = (int32_t)((dw2 >> 16) & 0xFFu);
+                const int32_t adv2 = 3 + lit2 + (int32_t)mlx2;
+                const int32_t ml2 = mlc2 + 4 + (mlx2 ? ext2 : 0);
+                // the same tests as the first; all its bytes lie in w|w2
+                // (p2 + 3 <= 31) and inside the ring
+                const bool ok2 = ok & (p2 + 3u <= 31u) & (ip2 + 16 <= wb + kPW) & (lit2 <= 12) &
+                                 !(mlx2 & (ext2 == 255)) & (ip2 + 1 <= iend - 17) & (!mlx2 | (ip2 + adv2 <= iend - 4)) &
+                                 (off2 != 0) & (off2 <= op2 + lit2) & (op2 + lit2 + ml2 < oend - 64) &
+                                 (k + 1 - kf < kPStage - 1);
+                // slot k + 1 is free when the first is taken (then k - kf <= 30);
+                // otherwise slot k is, and nothing is taken
+                stg[(ok ? k + 1 : k) & (kPStage - 1)] = (uint8_t)adv2;
+                ip += (ok ? adv : 0) + (ok2 ? adv2 : 0);
+                op += (ok ? lit + ml : 0) + (ok2 ? lit2 + ml2 : 0);
+                k += (int32_t)ok + (int32_t)ok2;
+#else
                 ip += ok ? adv : 0;
                 op += ok ? lit + ml : 0;
                 k += (int32_t)ok;
+#endif
                 need = !ok;
             }
         }
@@ -462,6 +507,9 @@ constexpr int32_t kRowsH = LZ4M_ROWS_H;
 #endif
 #ifndef LZ4M_ROWS_PUTMASK
 #define LZ4M_ROWS_PUTMASK 3   // 0 = branch-free dummy-slot puts (round 2); 1 = pass puts exec-masked; 2 = literal puts too; 3 = the whole pass body masked to the ready lanes
+#endif
+#ifndef LZ4M_ROWS_COUNTED
+#define LZ4M_ROWS_COUNTED 1   // every round issues a fixed number of memory operations on the common path (see the flush)
 #endif
 constexpr int32_t kRowsHS = kRowsH + 32;   // buffer stride (16-byte reads past the end stay inside)
 constexpr int32_t kRowsKeep = kRowsH / 2;   // history kept on a rebase
@@ -499,13 +547,6 @@ __device__ __forceinline__ void load32(const uint8_t* s, int32_t t, int32_t iend
     b = t + 32 <= iend ? ld16(s + t + 16) : ld16_guarded(s + t + 16, iend - t - 16);
 }
 
-// the 4 bytes at k (0..28) of the 32-byte window a|b
-__device__ __forceinline__ uint32_t dword32(u32x4 a, u32x4 b, uint32_t k) {
-    const uint32_t q = k >> 2;
-    const uint32_t lo = q == 0 ? a.x : q == 1 ? a.y : q == 2 ? a.z : q == 3 ? a.w : q == 4 ? b.x : q == 5 ? b.y : q == 6 ? b.z : b.w;
-    const uint32_t hi = q == 0 ? a.y : q == 1 ? a.z : q == 2 ? a.w : q == 3 ? b.x : q == 4 ? b.y : q == 5 ? b.z : q == 6 ? b.w : 0u;
-    return __builtin_amdgcn_alignbyte(hi, lo, k & 3);
-}
 
 // Period-`off` pattern of the first off (1..15) bytes of w, E[j] = w[j % off]:
 // per output dword, v_perm from bytes 0-7 and from bytes 8-15 with
@@ -570,6 +611,9 @@ __device__ __forceinline__ void parse_round(PSeq& P, int32_t jj, int32_t r, int3
                 ml += (int32_t)b;
             } while (b == 255 && pe < iend - t);
         }
+#if LZ4M_ROWS_COUNTED
+        wait_vm0();   // rare: so that no later use of off / ml waits on every path
+#endif
     }
     ml += 4;
     const int32_t len = act && !esc ? lit + ml : 0;
@@ -651,6 +695,9 @@ __global__ __launch_bounds__(64) void rows_exec_kernel(const uint8_t* __restrict
         psel[e] = v;
     }
     lds_cu32* PS = (lds_cu32*)psel;
+    // this lane's dummy store target (flush stores of lanes with nothing final)
+    uint8_t* const dst_dummy = reinterpret_cast<uint8_t*>(ctr) + kRowsDummy + 1024 * (blockIdx.x % kRowsDummySlots) + 16 * lane;
+    (void)dst_dummy;
     // row state (uniform across the row's 16 lanes)
     const uint8_t* s = nullptr;
     uint8_t* d = nullptr;
@@ -686,6 +733,9 @@ __global__ __launch_bounds__(64) void rows_exec_kernel(const uint8_t* __restrict
             k0 = ip = op = base = F = 0;
             have = true;
             sync = true;
+#if LZ4M_ROWS_COUNTED
+            wait_vm0();   // (once per block) no use of the row's state waits on the common path
+#endif
         }
         RP_MARK(8);
         if (sync) {   // block start, or the last round stopped early: parse this round now
@@ -700,12 +750,18 @@ __global__ __launch_bounds__(64) void rows_exec_kernel(const uint8_t* __restrict
             load_in(s, tn, iend, na, nb);
             dnn = load_len(dl, k0 + 32 + jj, nseq);
             sync = false;
+#if LZ4M_ROWS_COUNTED
+            wait_vm0();   // (rare: block starts, short rounds) the common path's waits stay counted
+#endif
         }
         if (P.use == 0) {
             sync = true;
             if (k0 >= nseq) {   // the block's good prefix is done: flush the rest exactly
                 for (int32_t c = F + 16 * jj; c < op; c += 256) gbl_put(d + c, lds_ld16(HB + (c - base)), op - c);
                 have = false;
+#if LZ4M_ROWS_COUNTED
+                wait_vm0();
+#endif
                 RP_MARK(20);
                 continue;
             }
@@ -746,6 +802,9 @@ __global__ __launch_bounds__(64) void rows_exec_kernel(const uint8_t* __restrict
             // op < oend - 64: the 16-byte reads stay inside the block's slot
             for (int32_t c = base + 16 * jj; c < op; c += 256) lds_st16(HB + (c - base), ld16(d + c));
             F = op;
+#if LZ4M_ROWS_COUNTED
+            wait_vm0();
+#endif
             RP_COUNT(25, 1);
             RP_MARK(21);
             continue;
@@ -782,6 +841,9 @@ __global__ __launch_bounds__(64) void rows_exec_kernel(const uint8_t* __restrict
                 lds_put(HB + (o - base + 16), P.x1, lit - 16);
             } else {   // a literal beyond the bytes at hand: from HBM (inside the block: good)
                 for (int32_t i = 16; i < lit; i += 16) lds_put(HB + (o - base + i), ld16(s + P.t + P.lp + i), lit - i);
+#if LZ4M_ROWS_COUNTED
+                wait_vm0();
+#endif
             }
         }
         RP_MARK(12);
@@ -789,9 +851,12 @@ __global__ __launch_bounds__(64) void rows_exec_kernel(const uint8_t* __restrict
         // the round writes into its source [s0, se)
         const bool far = (P.fl & kFlFar) != 0, late = (P.fl & kFlLate) != 0;
         u32x4 g0 = P.pre0;
-        if (__any(late)) {   // a source flushed only by the previous round (rare): load it now
+            if (__any(late)) {   // a source flushed only by the previous round (rare): load it now
             const u32x4 lv = ld16(d + (late ? s0 : 0));
             g0 = late ? lv : g0;
+#if LZ4M_ROWS_COUNTED
+            wait_vm0();
+#endif
         }
         const int32_t se = s0 + (off < ml ? off : ml);
         const bool per = off < 16;   // period pattern (s0 >= base here: m - base >= off)
@@ -858,7 +923,24 @@ __global__ __launch_bounds__(64) void rows_exec_kernel(const uint8_t* __restrict
         RP_MARK(13);
         // ---- flush, advance, rebase for the next round
         const int32_t opn = P.opn;
+#if LZ4M_ROWS_COUNTED
+        // exactly one store per lane and round, always issued (a lane with no
+        // complete chunk stores to its dummy slot), so the compiler counts the
+        // next round's waits instead of draining these stores (gfx9 counts
+        // stores in vmcnt); more than 256 pending bytes in a row is rare
+        {
+            const int32_t c = F + 16 * jj;
+            const bool fin = c + 16 <= opn;
+            const u32x4 v = lds_ld16(HB + (fin ? c - base : 0));
+            st16(fin ? d + c : dst_dummy, v);
+            if (__any(F + 256 + 16 <= opn)) {
+                for (int32_t c2 = c + 256; c2 + 16 <= opn; c2 += 256) st16(d + c2, lds_ld16(HB + (c2 - base)));
+                wait_vm0();
+            }
+        }
+#else
         for (int32_t c = F + 16 * jj; c + 16 <= opn; c += 256) st16(d + c, lds_ld16(HB + (c - base)));
+#endif
         F += (opn - F) & ~15;
         op = opn;
         ip = P.ipn;
@@ -966,8 +1048,6 @@ __device__ __forceinline__ void wave_copy_match(uint8_t* d, int32_t off, int32_t
 
 constexpr uint32_t kQFar = 1, kQFar1 = 2, kQLitHbm = 4;
 
-// s_waitcnt vmcnt(0) (expcnt and lgkmcnt left at their maximum)
-__device__ __forceinline__ void wait_vm0() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 
 // Pin values in registers at this point (no code): what is computed from a
 // loaded operand is materialised before the next load of that operand, so

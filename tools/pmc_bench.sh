@@ -22,4 +22,4 @@ WRITE_SIZE
 TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum
 TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum TCC_EA0_RDREQ_DRAM_sum TCC_HIT_sum
 GROUPS
-python3 "$REPO/tools/pmc_report.py" "$OUT" "$OUT/pmc_decompress.json" 1048576 4096 > "$OUT/report.json"
+python3 "$REPO/tools/pmc_report.py" "$OUT" "$OUT/pmc_decompress.json" 1048576 4096 "${CAL:-}" > "$OUT/report.json"

@@ -31,9 +31,18 @@ for f in sorted(glob.glob(f"{d}/p*/p*_counter_collection.csv")):
 out = {k: v for k, v in sorted(per.items())}
 print(json.dumps(out, indent=1))
 
-# ---- HBM bytes per launch (guide: separate passes; request-size counters,
-# calibrated here on the random-data dispatch whose bytes are known) ----
+# ---- HBM bytes per launch, the MI355X guide's method (MI355X_MICROARCH.md,
+# HBM section): separate --pmc passes; read = 2 x FETCH_SIZE (gfx950 tallies
+# 128-B requests at 64 B), write = WRITE_SIZE (exact for 16-B-per-lane
+# stores).  The request-size breakdown (RDREQ_32B/64B/128B, WRREQ_64B) is kept
+# for reference only: its write estimate read 0.75x the known bytes of a
+# streaming dispatch.  tools/pmc_cal.sh checks both methods on kernels of
+# known bytes in the decoder's access shapes (profiles/r03/*calibration*).
 def hbm_bytes(c):
+    return 2 * 1024 * c.get("FETCH_SIZE", 0), 1024 * c.get("WRITE_SIZE", 0)
+
+
+def hbm_bytes_reqsize(c):
     rd = 32 * c.get("TCC_EA0_RDREQ_32B_sum", 0) + 64 * c.get("TCC_EA0_RDREQ_64B_sum", 0) \
         + 128 * c.get("TCC_EA0_RDREQ_128B_sum", 0)
     wr = 64 * c.get("TCC_EA0_WRREQ_64B_sum", 0) + 32 * (c.get("TCC_EA0_WRREQ_sum", 0) - c.get("TCC_EA0_WRREQ_64B_sum", 0))
@@ -56,13 +65,21 @@ if len(sys.argv) > 2:
         "fetch_size_kb": head.get("FETCH_SIZE"),
         "write_size_kb": head.get("WRITE_SIZE"),
         "l2_hit": head.get("TCC_HIT_sum"),
-        "method": "read = 32*RDREQ_32B + 64*RDREQ_64B + 128*RDREQ_128B, write = 64*WRREQ_64B + 32*(WRREQ - WRREQ_64B); "
-                  "FETCH_SIZE reads exactly half of this (MI355X guide: 128-B requests tallied at 64 B)",
+        "method": "read = 2 x FETCH_SIZE, write = WRITE_SIZE (MI355X guide, HBM section; one counter group per "
+                  "rocprofv3 --pmc pass); calibrated on known-bytes kernels by tools/pmc_cal.sh",
+        "reqsize_method_read_bytes": hbm_bytes_reqsize(head)[0],
+        "reqsize_method_write_bytes": hbm_bytes_reqsize(head)[1],
     }
+    cal = sys.argv[5] if len(sys.argv) > 5 else None
+    if cal and os.path.exists(cal):
+        summary["calibration"] = {k: {m: v.get(m + "_ratio") for m in ("fetch2", "rdreq_sized", "write_size",
+                                                                        "wrreq_sized")}
+                                  for k, v in json.load(open(cal)).items()}
     if rand:
         rrd, rwr = hbm_bytes(rand)
-        summary["calibration_random_dispatch"] = {"read_bytes": rrd, "write_bytes": rwr,
-                                                 "note": "131072 random blocks: expected read ~= compressed bytes "
-                                                         "(~8.62e9), write = 131072 * 65536 = 8.59e9"}
+        summary["random_dispatch"] = {"read_bytes": rrd, "write_bytes": rwr,
+                                      "note": "131072 random (stored-like) blocks: the finisher's lane-per-block "
+                                              "literal copies; write = 131072 * 65536 = 8.59e9 bytes must leave, "
+                                              "reads ~= 8.62e9 compressed bytes plus any line re-fetches"}
     with open(sys.argv[2], "w") as f:
         json.dump(summary, f, indent=1)
