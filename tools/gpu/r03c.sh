@@ -1,21 +1,20 @@
-# r03c: GPU suite on the new default (counted waits + paired parse), A/B of
-# both changes with per-kernel times, phase split, SQ counters per sequence,
-# counter calibration and the decoder's HBM traffic (calibrated method)
+# r03c: LDS alignment micro-benchmark; parity of the aligned-LDS executor
+# variants; decoder A/B with per-kernel times (rocprofv3 stats); phase split
 export TMPDIR=/tmp
 O=gpurun_out/r03c
 mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/gpu_tests.log 2>&1; rc=$?
-tail -2 $O/gpu_tests.log
-if [ $rc -ne 0 ]; then exit $rc; fi
-for V in default p0 c0; do
+timeout -k 10 120 tools/micro/lds_align > $O/lds_align.log 2>&1 || exit $?
+for V in al al3; do
+  LZ4M_LIB=$PWD/tools/_abv/$V/_lz4m.so timeout -k 10 600 python -u -m pytest tests/test_gpu_codec.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider -k "decompress and (rows or auto)" > $O/tests_$V.log 2>&1 || { tail -30 $O/tests_$V.log; exit 1; }
+done
+for V in default al al3 n1 p0 c0; do
   L=""; [ $V != default ] && L=$PWD/tools/_abv/$V/_lz4m.so
   LZ4M_LIB=$L DECS=rows NBLK=1048576 REPS=3 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kt_$V -o kt -- python3 tools/probe_rows.py > $O/probe_$V.log 2>&1 || exit $?
-  tail -1 $O/probe_$V.log
+  find $O/kt_$V -type f ! -name "*kernel_stats.csv" -delete
 done
 LZ4M_LIB=$PWD/tools/_prof/_lz4m_rprof.so NB=262144 timeout -k 10 200 python3 -u tools/prof_rows.py > $O/rows_phases.log 2>&1 || exit $?
-cat $O/rows_phases.log
-DECS=rows NBLK=262144 REPS=1 timeout -k 10 400 bash tools/pmc_groups.sh $O/sq "rows_exec_kernel|rows_parse_kernel" tools/pmc/sq_exec.txt tools/probe_rows.py > $O/sq.log 2>&1 || exit $?
-LZ4M_LIB=$PWD/tools/_abv/c0/_lz4m.so DECS=rows NBLK=262144 REPS=1 timeout -k 10 400 bash tools/pmc_groups.sh $O/sq_c0 "rows_exec_kernel|rows_parse_kernel" tools/pmc/sq_exec.txt tools/probe_rows.py > $O/sq_c0.log 2>&1 || exit $?
-timeout -k 10 300 bash tools/pmc_cal.sh $O/cal > $O/cal.log 2>&1; echo cal=$?
-CAL=$PWD/$O/cal/calibration.json timeout -k 10 900 bash tools/pmc_bench.sh $O/pmc > $O/pmc.log 2>&1; echo pmc=$?
-cat $O/pmc/pmc_decompress.json
+echo "=== summary"
+tail -3 $O/tests_al.log | head -2; tail -1 $O/tests_al3.log
+for V in default al al3 n1 p0 c0; do echo "$V: $(grep -o '"silesia/rows": {[^}]*}' $O/probe_$V.log)"; find $O/kt_$V -name "*kernel_stats.csv" -exec grep -h -E "rows_parse|rows_exec|decompress_kernel" {} + | cut -d, -f1-5; done
+grep -E "mskor|misalign\": 0|misalign\": 1," $O/lds_align.log
+cat $O/rows_phases.log | tail -14
