@@ -107,6 +107,75 @@ __device__ __forceinline__ u32x4 period_pattern(u32x4 w, uint32_t off) {
     return u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
 }
 
+// ---------------------------------------------------- aligned LDS access
+// A _b64 / _b128 LDS access off its natural alignment -- and a _b32 one off
+// 4 bytes -- replays at ~56 cycles per wave-instruction on gfx950
+// (tools/micro/lds_align.hip; cdna_hip_programming.md Guideline 17), and the
+// decoders' history buffers are read and written at arbitrary byte offsets.
+#ifndef LZ4M_LDS_ALIGN
+#define LZ4M_LDS_ALIGN 0
+#endif
+// LZ4M_LDS_ALIGN: history accesses at arbitrary byte offsets made of
+// naturally aligned LDS accesses only.  A 16-byte read is three aligned
+// 8-byte reads and a funnel shift; an exact put of k <= 16 bytes is five
+// ds_mskor_b32 (dst = dst & ~mask | data) on the enclosing aligned dwords --
+// atomic per dword, so neighbouring sequences that share a boundary dword
+// can be written by one instruction -- with the masks from a table by
+// (address & 3, k).
+typedef __attribute__((address_space(3))) volatile uint64_t lds_vu64;
+typedef __attribute__((address_space(3))) const uint32_t lds_cu32;
+__device__ __forceinline__ uint32_t lds_addr(const lds_u8* p) { return (uint32_t)(uintptr_t)p; }
+__device__ __forceinline__ u32x4 lds_ld16a(const lds_u8* p) {
+    const uint32_t a = lds_addr(p);
+    const lds_vu64* q = (const lds_vu64*)(p - (a & 7u));
+    const uint64_t x0 = q[0], x1 = q[1], x2 = q[2];
+    const bool h = (a & 4u) != 0;
+    const uint32_t r = a & 3u;
+    const uint32_t c0 = (uint32_t)x0, c1 = (uint32_t)(x0 >> 32), c2 = (uint32_t)x1, c3 = (uint32_t)(x1 >> 32),
+                   c4 = (uint32_t)x2, c5 = (uint32_t)(x2 >> 32);
+    const uint32_t e0 = h ? c1 : c0, e1 = h ? c2 : c1, e2 = h ? c3 : c2, e3 = h ? c4 : c3, e4 = h ? c5 : c4;
+    return u32x4{__builtin_amdgcn_alignbyte(e1, e0, r), __builtin_amdgcn_alignbyte(e2, e1, r),
+                 __builtin_amdgcn_alignbyte(e3, e2, r), __builtin_amdgcn_alignbyte(e4, e3, r)};
+}
+#define LZ4M_MSKOR(addr, off, m, x) \
+    asm volatile("ds_mskor_b32 %0, %1, %2 offset:" #off ::"v"(addr), "v"(m), "v"((x) & (m)) : "memory")
+// byte masks of an exact put of k (0..16) bytes at address & 3 == r over the
+// enclosing dwords 0..3: table entry (r * 17 + k), 16 bytes (dword 4 is
+// computed); built once per workgroup by lds_put_table_init
+constexpr int kPutTab = 4 * 17 * 4;
+__device__ __forceinline__ void lds_put_table_init(uint32_t* tab, uint32_t lane, uint32_t nlanes) {
+    for (uint32_t e = lane; e < (uint32_t)kPutTab; e += nlanes) {
+        const uint32_t i = e & 3u, ent = e >> 2, k = ent % 17u, r = ent / 17u;
+        uint32_t m = 0;
+        for (uint32_t b = 0; b < 4; ++b) {
+            const uint32_t pos = 4u * i + b;   // byte of the 16..20-byte span
+            if (pos >= r && pos < r + k) m |= 0xFFu << (8 * b);
+        }
+        tab[e] = m;
+    }
+}
+__device__ __forceinline__ void lds_put_al(lds_u8* p, u32x4 v, int32_t k, lds_cu32* tab) {
+    const uint32_t a = lds_addr(p), r = a & 3u;
+    const uint32_t kk = k >= 16 ? 16u : (uint32_t)k;
+    const uint32_t s = (4u - r) & 3u;
+    const bool z = r == 0;
+    const uint32_t d0 = __builtin_amdgcn_alignbyte(v.x, z ? v.x : 0u, s);
+    const uint32_t d1 = __builtin_amdgcn_alignbyte(v.y, z ? v.y : v.x, s);
+    const uint32_t d2 = __builtin_amdgcn_alignbyte(v.z, z ? v.z : v.y, s);
+    const uint32_t d3 = __builtin_amdgcn_alignbyte(v.w, z ? v.w : v.z, s);
+    const uint32_t d4 = __builtin_amdgcn_alignbyte(0u, z ? 0u : v.w, s);
+    u32x4 m;
+    __builtin_memcpy(&m, (const uint8_t*)(tab + 4u * (r * 17u + kk)), 16);   // 16-byte aligned
+    const int32_t t4 = (int32_t)(r + kk) - 16;   // bytes in dword 4 (0..3)
+    const uint32_t m4 = t4 > 0 ? (1u << (8 * t4)) - 1u : 0u;
+    const uint32_t b4 = a & ~3u;
+    LZ4M_MSKOR(b4, 0, m.x, d0);
+    LZ4M_MSKOR(b4, 4, m.y, d1);
+    LZ4M_MSKOR(b4, 8, m.z, d2);
+    LZ4M_MSKOR(b4, 12, m.w, d3);
+    LZ4M_MSKOR(b4, 16, m4, d4);
+}
+
 __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 
 __device__ __forceinline__ int64_t readlane64(int64_t v, int lane) {

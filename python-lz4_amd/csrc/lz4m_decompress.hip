@@ -787,6 +787,17 @@ __global__ __launch_bounds__(256, 4) void hist_decompress_kernel(const uint8_t* 
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     lds_u8* IN = (lds_u8*)ins[wv];
     lds_u8* OB = (lds_u8*)outs[wv];
+#if LZ4M_LDS_ALIGN
+    __shared__ __attribute__((aligned(16))) uint32_t mtab[kPutTab];
+    lds_put_table_init(mtab, threadIdx.x, 256);
+    __syncthreads();
+    lds_cu32* MT = (lds_cu32*)mtab;
+#define HPUT(p, v, k) lds_put_al((p), (v), (k), MT)
+#define HLD(p) lds_ld16a(p)
+#else
+#define HPUT(p, v, k) lds_put_exact((p), (v), (k))
+#define HLD(p) lds_ld16(p)
+#endif
     HP_DECL
     for (int64_t b = (int64_t)blockIdx.x * 4 + wv; b < n; b += (int64_t)gridDim.x * 4) {
         const uint8_t* s = src + src_off[b];
@@ -836,8 +847,8 @@ __global__ __launch_bounds__(256, 4) void hist_decompress_kernel(const uint8_t* 
             // so the chain costs six dependent gathers.
             while (nseq < 64 && pos + 144 <= kCoopIn) {
                 const int32_t ta = pos + (int32_t)lane, tb = ta + 64;
-                const CoopSeq qa = coop_parse(IN, ta, lds_ld16(IN + ta));
-                const CoopSeq qb = coop_parse(IN, tb, lds_ld16(IN + tb));
+                const CoopSeq qa = coop_parse(IN, ta, HLD(IN + ta));
+                const CoopSeq qb = coop_parse(IN, tb, HLD(IN + tb));
                 const uint64_t sa = __ballot(qa.simple), sb = __ballot(qb.simple);
                 constexpr int32_t kNoSeq = 1023;
                 int32_t ja = qa.simple ? (int32_t)lane + qa.adv : kNoSeq;
@@ -923,7 +934,7 @@ __global__ __launch_bounds__(256, 4) void hist_decompress_kernel(const uint8_t* 
             // sequence k in lane k
             const bool act = (int)lane < nseq;
             const int32_t tk = act ? myseq : 0;
-            const u32x4 w = lds_ld16(IN + tk);
+            const u32x4 w = HLD(IN + tk);
             const CoopSeq q = coop_parse(IN, tk, w);
             const int32_t lit = q.lit, off = q.off, ml = q.ml, adv = q.adv;
             const int32_t len = act ? lit + ml : 0;
@@ -956,10 +967,10 @@ __global__ __launch_bounds__(256, 4) void hist_decompress_kernel(const uint8_t* 
             if (far) pre = ld16(d + (m - off) + (DICT && m - off < 0 ? ddelta : 0));
             if (u && lit > 0) {
                 if (lit <= 12) {
-                    lds_put_exact(OB + (o - base), window_shift1(w), lit);
+                    HPUT(OB + (o - base), window_shift1(w), lit);
                 } else {
                     for (int32_t i = 0; i < lit; i += 16)
-                        lds_put_exact(OB + (o - base + i), lds_ld16(IN + q.litpos + i), lit - i);
+                        HPUT(OB + (o - base + i), HLD(IN + q.litpos + i), lit - i);
                 }
             }
             lds_wait();
@@ -989,14 +1000,14 @@ __global__ __launch_bounds__(256, 4) void hist_decompress_kernel(const uint8_t* 
                         for (int32_t i = 0; i < ml; i += 16) {
                             const int32_t sp = s0 + i;   // < base: flushed long ago (base <= F - 4 K)
                             const u32x4 v = (i == 0 && far)   ? pre
-                                            : sp >= base          ? lds_ld16(OB + (sp - base))
+                                            : sp >= base          ? HLD(OB + (sp - base))
                                                                   : ld16(d + sp + (DICT && sp < 0 ? ddelta : 0));
-                            lds_put_exact(OB + (m - base + i), v, ml - i);
+                            HPUT(OB + (m - base + i), v, ml - i);
                         }
                     } else {   // s0 > m - 16 >= base
-                        const u32x4 pat = period_pattern(lds_ld16(OB + (s0 - base)), (uint32_t)off);
+                        const u32x4 pat = period_pattern(HLD(OB + (s0 - base)), (uint32_t)off);
                         const int32_t step = 16 - (16 % off);
-                        for (int32_t i = 0; i < ml; i += step) lds_put_exact(OB + (m - base + i), pat, ml - i);
+                        for (int32_t i = 0; i < ml; i += step) HPUT(OB + (m - base + i), pat, ml - i);
                     }
                 }
                 lds_wait();
@@ -1023,6 +1034,8 @@ __global__ __launch_bounds__(256, 4) void hist_decompress_kernel(const uint8_t* 
         HP_COUNT(11, 1);
     }
     HP_FLUSH();
+#undef HPUT
+#undef HLD
 }
 
 // Linked-block frames (lz4frame.c:1853-1856, LZ4F_updateDict): block i may
