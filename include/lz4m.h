@@ -137,7 +137,6 @@ const char* lz4m_version_string(void);
  *             lz4m_decompress_workspace_size);
  *   hist   -- one wavefront per block with its recent output in LDS (small and
  *             mid-size batches, large blocks, and any batch without scratch);
- *   quad   -- an experimental 4-lane-per-block executor (A/B measurements only).
  * This entry point takes no scratch, so it always uses the hist decoder; pass
  * scratch through lz4m_decompress_batch_ws for the rows decoder.
  */
@@ -160,18 +159,17 @@ size_t lz4m_decompress_workspace_size(int64_t n, int64_t src_bytes);
  * at least lz4m_decompress_workspace_bytes(), not shared with a concurrently
  * running call).  Picks the decoder by batch size and scratch: rows from
  * LZ4M_ROWS_MIN_BLOCKS (32 768) blocks when the scratch fits, else hist
- * (env LZ4M_DECODER=rows|hist|quad forces one). */
+ * (env LZ4M_DECODER=rows|hist forces one). */
 int lz4m_decompress_batch_ws(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len,
                              uint8_t* d_dst, const int64_t* d_dst_off, const int32_t* d_dst_cap,
                              int32_t* d_status, int64_t n, void* d_work, size_t work_bytes,
                              lz4m_stream_t stream);
 
 /* lz4m_decompress_batch_ws with an explicit decoder (tests, A/B runs); any
- * other id (1, 2 and 5 were retired decoders) returns LZ4M_EINVAL. */
+ * other id (1, 2, 5 and 6 were retired decoders) returns LZ4M_EINVAL. */
 #define LZ4M_DECODER_AUTO   0
 #define LZ4M_DECODER_HIST   3
 #define LZ4M_DECODER_ROWS   4
-#define LZ4M_DECODER_QUAD   6
 int lz4m_decompress_batch_sel(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len,
                               uint8_t* d_dst, const int64_t* d_dst_off, const int32_t* d_dst_cap,
                               int32_t* d_status, int64_t n, void* d_work, size_t work_bytes, int decoder,

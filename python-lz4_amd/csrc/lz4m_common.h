@@ -113,7 +113,7 @@ __device__ __forceinline__ u32x4 period_pattern(u32x4 w, uint32_t off) {
 // (tools/micro/lds_align.hip; cdna_hip_programming.md Guideline 17), and the
 // decoders' history buffers are read and written at arbitrary byte offsets.
 #ifndef LZ4M_LDS_ALIGN
-#define LZ4M_LDS_ALIGN 0
+#define LZ4M_LDS_ALIGN 1   // 0 = plain (unaligned) wide accesses; 2 = plain stores for wholly covered dwords
 #endif
 // LZ4M_LDS_ALIGN: history accesses at arbitrary byte offsets made of
 // naturally aligned LDS accesses only.  A 16-byte read is three aligned
@@ -169,11 +169,23 @@ __device__ __forceinline__ void lds_put_al(lds_u8* p, u32x4 v, int32_t k, lds_cu
     const int32_t t4 = (int32_t)(r + kk) - 16;   // bytes in dword 4 (0..3)
     const uint32_t m4 = t4 > 0 ? (1u << (8 * t4)) - 1u : 0u;
     const uint32_t b4 = a & ~3u;
+#if LZ4M_LDS_ALIGN >= 2
+    // a dword the put covers wholly is owned by this lane: a plain aligned
+    // store (about half a masked OR's LDS time); partial ones are masked ORs
+    lds_u8* q = p - r;
+    typedef __attribute__((address_space(3))) volatile uint32_t vu32;
+    if (m.x == ~0u) { *(vu32*)q = d0; } else if (m.x) { LZ4M_MSKOR(b4, 0, m.x, d0); }
+    if (m.y == ~0u) { *(vu32*)(q + 4) = d1; } else if (m.y) { LZ4M_MSKOR(b4, 4, m.y, d1); }
+    if (m.z == ~0u) { *(vu32*)(q + 8) = d2; } else if (m.z) { LZ4M_MSKOR(b4, 8, m.z, d2); }
+    if (m.w == ~0u) { *(vu32*)(q + 12) = d3; } else if (m.w) { LZ4M_MSKOR(b4, 12, m.w, d3); }
+    if (m4) LZ4M_MSKOR(b4, 16, m4, d4);
+#else
     LZ4M_MSKOR(b4, 0, m.x, d0);
     LZ4M_MSKOR(b4, 4, m.y, d1);
     LZ4M_MSKOR(b4, 8, m.z, d2);
     LZ4M_MSKOR(b4, 12, m.w, d3);
     LZ4M_MSKOR(b4, 16, m4, d4);
+#endif
 }
 
 __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }

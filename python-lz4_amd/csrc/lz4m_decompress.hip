@@ -752,6 +752,43 @@ __device__ __forceinline__ void lds_put_exact(lds_u8* p, u32x4 v, int32_t k) {
 
 __device__ __forceinline__ void lds_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
+// A length-byte run read 32 bytes per memory round trip (wave-uniform; the
+// one-sequence path of a long literal, e.g. the 257 length bytes of a stored-
+// looking 64 KiB block): the same outcome as the byte loop
+//   do { x = s[q++]; len += x; } while (x == 255 && q < lim)   (entered with q < lim)
+// -- true with q past the first byte < 255 if that byte lies before lim, else
+// false (the caller then leaves the sequence to the exact path).
+__device__ __forceinline__ bool run_len32(const uint8_t* s, int32_t& q, int32_t lim, int32_t iend, int32_t& len) {
+    while (q < lim) {
+        u32x4 v[2];
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const int32_t x = q + 16 * c;
+            v[c] = x + 16 <= iend ? ld16(s + x) : ld16_guarded(s + x, iend - x);
+        }
+        int32_t j = 32;   // first byte != 255 of the 32
+#pragma unroll
+        for (int c = 1; c >= 0; --c) {
+            const uint32_t n0 = ~v[c].x, n1 = ~v[c].y, n2 = ~v[c].z, n3 = ~v[c].w;
+            const int32_t w = n0 ? 0 : n1 ? 1 : n2 ? 2 : n3 ? 3 : 4;
+            if (w < 4) {
+                const uint32_t nw = w == 0 ? n0 : w == 1 ? n1 : w == 2 ? n2 : n3;
+                j = 16 * c + 4 * w + (int32_t)(__builtin_ctz(nw) >> 3);
+            }
+        }
+        if (q + j >= lim) return false;   // no byte < 255 before lim
+        if (j < 32) {
+            const u32x4 vc = j < 16 ? v[0] : v[1];
+            len += 255 * j + (int32_t)byte_of(vc, j & 15);
+            q += j + 1;
+            return true;
+        }
+        len += 255 * 32;
+        q += 32;
+    }
+    return false;
+}
+
 // LZ4M_HIST_PROF (diagnostic builds only, tools/prof_hist.py): per-phase
 // cycle sums of hist_decompress_kernel, read with lz4m_hist_prof.
 #ifdef LZ4M_HIST_PROF
@@ -892,12 +929,8 @@ __global__ __launch_bounds__(256, 4) void hist_decompress_kernel(const uint8_t* 
                 const uint32_t tok = s[ip];
                 int32_t lit = (int32_t)(tok >> 4), ml = (int32_t)(tok & 15u), q = ip + 1;
                 if (lit == 15) {
-                    uint32_t x = 255;
-                    while (x == 255 && q < iend - 48) {
-                        x = s[q++];
-                        lit += (int32_t)x;
-                    }
-                    if (x == 255 || q + lit > iend - 32 || op + lit > oend - 32) break;   // lz4.c:2016-2027
+                    if (q >= iend - 48 || !run_len32(s, q, iend - 48, iend, lit)) break;
+                    if (q + lit > iend - 32 || op + lit > oend - 32) break;   // lz4.c:2016-2027
                 } else if (q > iend - 17) {
                     break;   // lz4.c:2034
                 }
@@ -905,12 +938,8 @@ __global__ __launch_bounds__(256, 4) void hist_decompress_kernel(const uint8_t* 
                 const int32_t off = (int32_t)s[q + lit] | ((int32_t)s[q + lit + 1] << 8);
                 int32_t qe = q + lit + 2;
                 if (ml == 15) {
-                    uint32_t x = 255;
-                    while (x == 255 && qe < iend - 5) {
-                        x = s[qe++];
-                        ml += (int32_t)x;
-                    }
-                    if (x == 255 || qe > iend - 5) break;
+                    if (qe >= iend - 5 || !run_len32(s, qe, iend - 5, iend, ml)) break;
+                    if (qe > iend - 5) break;
                 }
                 ml += 4;
                 if (off < 1 || off > opm || opm + ml >= oend - 64) break;
@@ -1135,19 +1164,18 @@ int env_int(const char* name, int dflt) {
     return v > 0 ? v : dflt;
 }
 
-// the values are the C-ABI's decoder ids (include/lz4m.h); 1, 2 and 5 were
-// retired decoders and are rejected
-enum Decoder { kAuto = 0, kHistDec = 3, kRowsDec = 4, kQuadDec = 6 };
+// the values are the C-ABI's decoder ids (include/lz4m.h); 1, 2, 5 and 6
+// were retired decoders and are rejected
+enum Decoder { kAuto = 0, kHistDec = 3, kRowsDec = 4 };
 
-// LZ4M_DECODER forces a decoder (A/B measurements, tests): hist | rows |
-// quad; unset = by batch size and scratch.
+// LZ4M_DECODER forces a decoder (A/B measurements, tests): hist | rows;
+// unset = by batch size and scratch.
 int decoder_env() {
     static const int mode = [] {
         const char* e = getenv("LZ4M_DECODER");
         if (e == nullptr) return (int)kAuto;
         if (strcmp(e, "hist") == 0) return (int)kHistDec;
         if (strcmp(e, "rows") == 0) return (int)kRowsDec;
-        if (strcmp(e, "quad") == 0) return (int)kQuadDec;
         return (int)kAuto;
     }();
     return mode;
@@ -1167,7 +1195,7 @@ extern "C" int lz4m_decompress_batch_sel(const uint8_t* d_src, const int64_t* d_
                                          uint8_t* d_dst, const int64_t* d_dst_off, const int32_t* d_dst_cap,
                                          int32_t* d_status, int64_t n, void* d_work, size_t work_bytes, int decoder,
                                          lz4m_stream_t stream) {
-    if (n < 0 || !(decoder == kAuto || decoder == kHistDec || decoder == kRowsDec || decoder == kQuadDec))
+    if (n < 0 || !(decoder == kAuto || decoder == kHistDec || decoder == kRowsDec))
         return LZ4M_EINVAL;
     if (n == 0) return 0;
     hipStream_t st = (hipStream_t)stream;
@@ -1182,12 +1210,11 @@ extern "C" int lz4m_decompress_batch_sel(const uint8_t* d_src, const int64_t* d_
     static const int rows_min = env_int("LZ4M_ROWS_MIN_BLOCKS", 32768);   // crossover measured, DESIGN 3.1
     if (decoder == kAuto) decoder = rows_fit && n >= rows_min ? kRowsDec : kHistDec;
     if (decoder != kHistDec && !rows_fit) decoder = kHistDec;
-    if (decoder == kRowsDec || decoder == kQuadDec) {
-        const int quad = decoder == kQuadDec;
+    if (decoder == kRowsDec) {
         int pg = 1, eg = 1;
-        lz4m_rows_grids(n, quad, &pg, &eg);
+        lz4m_rows_grids(n, &pg, &eg);
         const int rc = lz4m_rows_launch(d_src, d_src_off, d_src_len, d_dst, d_dst_off, d_dst_cap, n, d_work, work_bytes,
-                                        pg, eg, quad, st);
+                                        pg, eg, st);
         if (rc != 0) return rc;
         const RowMeta* meta = reinterpret_cast<const RowMeta*>(static_cast<const uint8_t*>(d_work) + kRowsMeta);
         const int64_t grid = (n + 255) / 256;

@@ -19,8 +19,8 @@ struct RowMeta {
 static_assert(sizeof(RowMeta) == 32, "RowMeta layout");
 
 // scratch layout: 64 bytes of counters, 256 KiB of dummy targets (the
-// unconditional loads / stores of lanes with nothing to load or store: 1 KiB
-// per wave slot, blockIdx % 256), one RowMeta per block, then the length bytes
+// unconditional flush stores of lanes with nothing final: 1 KiB per wave
+// slot, blockIdx % 256), one RowMeta per block, then the length bytes
 constexpr size_t kRowsDummy = 64;
 constexpr size_t kRowsDummySlots = 256;
 constexpr size_t kRowsMeta = kRowsDummy + kRowsDummySlots * 1024;
@@ -33,10 +33,9 @@ extern "C" {
 // scratch needed before the length bytes: 64 bytes of counters + one RowMeta per block
 size_t lz4m_rows_fixed_bytes(int64_t n);
 // persistent grid sizes for the two kernels on the current device
-int lz4m_rows_grids(int64_t n, int quad, int* parse_grid, int* exec_grid);
-// parse + row execution (quad: the quad executor, else the 16-lane row
-// executor); the finisher is launched by the caller afterwards
+int lz4m_rows_grids(int64_t n, int* parse_grid, int* exec_grid);
+// parse + row execution; the finisher is launched by the caller afterwards
 int lz4m_rows_launch(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len, uint8_t* d_dst,
                      const int64_t* d_dst_off, const int32_t* d_dst_cap, int64_t n, void* d_work, size_t work_bytes,
-                     int parse_grid, int exec_grid, int quad, hipStream_t stream);
+                     int parse_grid, int exec_grid, hipStream_t stream);
 }

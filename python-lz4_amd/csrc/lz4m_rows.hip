@@ -274,7 +274,7 @@ static_assert(kPStage == 32 || kPStage == 64, "length ring: 32 or 64 entries");
 #endif
 constexpr int kPWG = LZ4M_PARSE_WG;     // parse workgroup (LDS is allocated per workgroup)
 #ifndef LZ4M_PARSE_PAIR
-#define LZ4M_PARSE_PAIR 1               // the fast loop takes two sequences per step when it can
+#define LZ4M_PARSE_PAIR 0               // A/B: two sequences per fast step (measured -1.5 %)
 #endif
 #ifndef LZ4M_PARSE_MIN_ACTIVE
 #define LZ4M_PARSE_MIN_ACTIVE 40        // run the general step once fewer lanes than this can go on
@@ -552,7 +552,7 @@ constexpr int32_t kRowsH = LZ4M_ROWS_H;
 #define LZ4M_ROWS_PASS1 0     // A/B: a first readiness pass without the row scans (sources before the round)
 #endif
 #ifndef LZ4M_ROWS_COUNTED
-#define LZ4M_ROWS_COUNTED 1   // every round issues a fixed number of memory operations on the common path (see the flush)
+#define LZ4M_ROWS_COUNTED 0   // A/B: a fixed number of memory operations per round on the common path (measured -1 %)
 #endif
 constexpr int32_t kRowsHS = kRowsH + 32;   // buffer stride (16-byte reads past the end stay inside)
 constexpr int32_t kRowsKeep = kRowsH / 2;   // history kept on a rebase
@@ -1046,548 +1046,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LZ4M_ROWS_WA
     RP_FLUSH(8, 32);
 }
 
-// ----------------------------------------------------- 2b. quad execution
-// One QUAD (4 lanes) per block, 16 blocks per wave.  A round is the quad's
-// next 4 recorded sequences, lane t = sequence k + t: each lane decodes its
-// own sequence (quad prefix sums of the recorded lengths and of the decoded
-// lengths place it), and the round is then EXECUTED IN ORDER, one lane of
-// each quad at a time (4 sub-steps), with wild 16-byte LDS copies exactly as
-// the reference's own wild copies (lz4.c:2015-2023, :2052-2063): every byte a
-// sub-step writes past its sequence's end is rewritten by a later sub-step of
-// the same quad before anything reads it.  So there are no readiness passes
-// and no exact-length puts; a sub-step is one literal store, one source read
-// and one match store.  The output of each block is assembled in its quad's
-// LDS history ([base, base + kQH) of the block); older sources come from HBM
-// (the block's own flushed output), requested when the round is decoded.
-//
-// Stages run one round apart (software pipeline, per quad): lengths of round
-// R+3 are requested, round R+2's inputs (32 bytes per sequence) requested,
-// round R+1 decoded (its far sources requested), round R executed.
-#ifndef LZ4M_QUAD_H
-#define LZ4M_QUAD_H 1024
-#endif
-#ifndef LZ4M_QUAD_KEEP
-#define LZ4M_QUAD_KEEP (LZ4M_QUAD_H * 3 / 8)
-#endif
-#ifndef LZ4M_QUAD_ROOM
-#define LZ4M_QUAD_ROOM (LZ4M_QUAD_H / 8)
-#endif
-constexpr int32_t kQH = LZ4M_QUAD_H;        // history bytes per quad
-constexpr int32_t kQHS = kQH + 48;           // stride: wild stores past kQH stay in the quad's buffer
-constexpr int32_t kQKeep = LZ4M_QUAD_KEEP;   // history kept on a rebase
-constexpr int32_t kQRoom = LZ4M_QUAD_ROOM;   // rebase when less room than this is left
-static_assert(kQKeep % 16 == 0 && kQKeep >= 96 && kQKeep + kQRoom <= kQH && kQKeep <= 1024, "quad history");
-
-// lane J of each quad, to all 4 lanes (quad_perm [J,J,J,J])
-template <int J>
-__device__ __forceinline__ int32_t qbc(int32_t v) {
-    return __builtin_amdgcn_mov_dpp(v, J * 0x55, 0xF, 0xF, false);
-}
-// v of lane j (0..4) of each quad, 4 = `at4`
-__device__ __forceinline__ int32_t qsel(int32_t v, int32_t j, int32_t at4) {
-    const int32_t a = qbc<0>(v), b = qbc<1>(v), c = qbc<2>(v), e = qbc<3>(v);
-    return j == 0 ? a : j == 1 ? b : j == 2 ? c : j == 3 ? e : at4;
-}
-// exclusive prefix sum over the quad; `tot` = the quad's sum
-// (every DPP read is evaluated by all 4 lanes and selected after: inside a
-// conditional expression it would run with the source lane switched off)
-__device__ __forceinline__ int32_t quad_excl_sum(int32_t v, int32_t t, int32_t& tot) {
-    const int32_t x = __builtin_amdgcn_mov_dpp(v, 0x90, 0xF, 0xF, false);   // [0,0,1,2]
-    const int32_t a = v + (t >= 1 ? x : 0);
-    const int32_t y = __builtin_amdgcn_mov_dpp(a, 0x40, 0xF, 0xF, false);   // [0,0,0,1]
-    const int32_t b = a + (t >= 2 ? y : 0);
-    tot = qbc<3>(b);
-    return b - v;
-}
-
-// Wave-cooperative exact copies in HBM (64 lanes; lane = l), for sequences
-// that do not fit a quad's history.  Same semantics as row_copy_*.
-__device__ __forceinline__ void wave_copy_literal(uint8_t* d, const uint8_t* s, int32_t len, int32_t l) {
-    for (int32_t pos = 16 * l; pos < len; pos += 1024) {
-        const u32x4 v = len - pos >= 16 ? ld16(s + pos) : ld16_guarded(s + pos, len - pos);
-        gbl_put(d + pos, v, len - pos);
-    }
-}
-__device__ __forceinline__ void wave_copy_match(uint8_t* d, int32_t off, int32_t len, int32_t l) {
-    if (off <= 0) return;   // never for a recorded sequence (offset 0 goes to the exact path)
-    if (off >= 16) {
-        const int32_t w = (off < 1024 ? off : 1024) & ~15;   // a step's sources all precede it
-        for (int32_t b = 0; b < len; b += w) {
-            const int32_t pos = b + 16 * l;
-            if (16 * l < w && pos < len) gbl_put(d + pos, ld16(d + pos - off), len - pos);
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-        }
-        return;
-    }
-    const u32x4 pat = period_pattern(ld16(d - off), (uint32_t)off);
-    const int32_t step = 16 - (16 % off);
-    for (int32_t pos = step * l; pos < len; pos += step * 64) gbl_put(d + pos, pat, len - pos);
-}
-
-constexpr uint32_t kQFar = 1, kQFar1 = 2, kQLitHbm = 4;
-
-
-// Pin values in registers at this point (no code): what is computed from a
-// loaded operand is materialised before the next load of that operand, so
-// the old and new values never overlap and a loaded register is never copied
-// (a copy would wait for the load).
-#define QPIN4(v) asm volatile("" ::"v"((v).x), "v"((v).y), "v"((v).z), "v"((v).w) : "memory")
-#define QPIN(a, b, c, e) asm volatile("" ::"v"(a), "v"(b), "v"(c), "v"(e) : "memory")
-
-// A decoded round (one per lane: its sequence), waiting for execution.
-struct QRound {
-    bool v;
-    int32_t k, use, lit, off, ml, o, ip, lp, b, oEnd;
-    uint32_t fl;
-    u32x4 x0, g0, g1;   // literal bytes 0-15; far source bytes (requested at decode)
-};
-
-// Per iteration (software pipeline, per quad): decode round R+1 and request
-// its far sources, request round R+2's inputs and round R+3's length bytes,
-// THEN execute round R -- whose far sources were requested an iteration ago.
-// Every operand the pipeline loads (lenL, wa/wb, a round's g0/g1) is written
-// by exactly one UNCONDITIONAL load per iteration (lanes with nothing to load
-// read their dummy slot) and is never copied: the decoded rounds alternate
-// between two QRound slots (the loop body is unrolled twice), so nothing
-// waits for a load before the instruction that reads it.  Every other global
-// access of the common path is unconditional too (flush stores of lanes with
-// nothing final go to the dummy slot), so the compiler's counted waits are
-// the same on every path; the rare paths (a block grab, a sequence that does
-// not fit, a slow decode) end with a full wait.
-#ifndef LZ4M_QUAD_WAVES
-#define LZ4M_QUAD_WAVES 2   // waves per SIMD the register budget is sized for
-#endif
-__global__ __launch_bounds__(64, LZ4M_QUAD_WAVES) void quad_exec_kernel(const uint8_t* __restrict__ src,
-                                                       const int64_t* __restrict__ src_off,
-                                                       const int32_t* __restrict__ src_len, uint8_t* dst,
-                                                       const int64_t* __restrict__ dst_off,
-                                                       const RowMeta* __restrict__ meta,
-                                                       const uint8_t* __restrict__ lens, int64_t n,
-                                                       unsigned long long* __restrict__ ctr,
-                                                       uint8_t* __restrict__ dummy, uint32_t max_iters,
-                                                       int32_t* __restrict__ dbg) {
-    __shared__ __attribute__((aligned(16))) uint8_t hists[16 * kQHS];
-    __shared__ __attribute__((aligned(16))) uint8_t wins[16 * 128];
-    const int32_t lane = (int32_t)threadIdx.x;
-    const int32_t t = lane & 3;
-    lds_u8* const HB = (lds_u8*)(hists + (lane >> 2) * kQHS);
-    lds_u8* const WQ = (lds_u8*)(wins + (lane >> 2) * 128);   // the quad's input window
-    // the target of loads with nothing to load: one slot per wave (all its
-    // lanes read the same 16 bytes: one access) and read-only
-    const uint8_t* const dmy = dummy + 16 * (blockIdx.x & 63);
-    // ---- quad state (uniform across the quad's 4 lanes; valid pointers
-    // even before a block: the requests are unconditional)
-    const uint8_t* s = src;
-    uint8_t* d = dst;
-    const uint8_t* dl = lens;
-    int32_t iend = 0, nseq = 0, base = 0, F = 0;
-    bool have = false, done = false, wait_big = false;
-    // fronts: next lengths to request, input position of stage L, output
-    // position and history base after the rounds decoded so far
-    int32_t kF = 0, ipF = 0, oF = 0, bD = 0;
-    // stage L: a round's length bytes (lane t: sequence kL + t; the aligned
-    // dword holding it, in lenA or lenB)
-    bool vL = false;
-    int32_t kL = 0;
-    uint32_t lenA = 0, lenB = 0;
-    // prefetch touches: a dword 256 input bytes and 64 length bytes ahead,
-    // loaded into tA / tB (alternating) and folded into `junk` an iteration
-    // later, so the lines are in L2 when the window and length loads reach them
-    uint32_t tA = 0, tB = 0, junk = 0;
-    // stage I: a round's inputs (32 bytes per lane, in waA|wbA or waB|wbB)
-    bool vI = false;
-    int32_t kI = 0, ipI = 0, lenI = 0, ip0I = 0;
-    u32x4 waA = u32x4{0, 0, 0, 0}, wbA = waA, waB = waA, wbB = waA;
-    QRound R0, R1;
-    R0.v = R1.v = false;
-    R0.k = R0.use = R0.lit = R0.off = R0.ml = R0.o = R0.ip = R0.lp = R0.b = R0.oEnd = 0;
-    R0.fl = 0;
-    R0.x0 = R0.g0 = R0.g1 = waA;
-    R1 = R0;
-    uint32_t guard = 0;
-    RP_DECL
-    // one iteration: decode into Rd (inputs wa|wb, length dword lenX) and
-    // execute Rx, requesting the next inputs into na|nb and the next length
-    // dword into lenY; returns true when every quad is done
-    auto step = [&](QRound& Rx, QRound& Rd, const u32x4& wa0, const u32x4& wb0, u32x4& na, u32x4& nb,
-                    const uint32_t& lenX, uint32_t& lenY, const uint32_t& tX, uint32_t& tY) -> bool {
-        RP_MARK(15);
-        RP_COUNT(16, 1);
-        // ---- 1. quads without a block take the next ones (one atomic per wave)
-        if (__any(!have && !done)) {
-            const uint64_t want = __ballot(!have && !done && t == 0);
-            unsigned long long b0 = 0;
-            if (lane == 0) b0 = atomicAdd(&ctr[2], (unsigned long long)__popcll(want));
-            b0 = (unsigned long long)readlane64((int64_t)b0, 0);
-            if (!have && !done) {
-                const uint64_t below = want & ((1ull << (lane & 60)) - 1ull);
-                const unsigned long long b = b0 + (unsigned long long)__popcll(below);
-                if (b >= (unsigned long long)n) {
-                    done = true;
-                } else {
-                    const RowMeta mt = meta[b];
-                    if (mt.nseq > 0) {   // else the finisher decodes the whole block: take another
-                        s = src + src_off[b];
-                        d = dst + dst_off[b];
-                        iend = src_len[b];
-                        dl = lens + mt.loff;
-                        nseq = mt.nseq;
-                        base = F = kF = ipF = oF = bD = 0;
-                        have = true;
-                        wait_big = vL = vI = false;
-                        Rx.v = Rd.v = false;
-                    }
-                }
-            }
-            wait_vm0();
-        }
-        if (__all(done)) return true;
-        RP_MARK(8);
-        // ---- 2. decode stage I into Rd and request its far sources
-        {
-            // this lane's 32 input bytes: from the quad's 128-byte window
-            // (staged through LDS), or loaded by the lane itself near the
-            // block's end (the window would pass iend)
-            const bool wm = vI && ip0I + 128 <= iend;
-            lds_st16(WQ + 16 * t, wa0);
-            lds_st16(WQ + 64 + 16 * t, wb0);
-            const int32_t rel = ipI - ip0I;
-            const bool inw = rel <= 96;
-            u32x4 wa = lds_ld16(WQ + (wm && inw ? rel : 0));
-            u32x4 wb = lds_ld16(WQ + (wm && inw ? rel + 16 : 0));
-            wa = wm ? wa : wa0;
-            wb = wm ? wb : wb0;
-            const bool act = vI && kI + t < nseq;
-            if (wm && !inw && act) {   // a sequence more than 96 bytes past the round's first (rare)
-                wa = ld16(s + ipI);   // (good sequence: ipI + 16 < iend)
-                wb = ld16(s + (ipI + 32 <= iend ? ipI + 16 : iend - 16));
-                wait_vm0();
-            }
-            const bool esc = lenI == 255;   // length >= 255: the parse left it to be re-parsed
-            const bool wbok = ipI + 32 <= iend;
-            const uint32_t tok = wa.x & 0xFFu;
-            const int32_t lit0 = (int32_t)(tok >> 4);
-            const bool litx = lit0 == 15;
-            const int32_t lit = lit0 + (litx ? (int32_t)byte_of(wa, 1) : 0);
-            const int32_t lp = litx ? 2 : 1;
-            const int32_t po = lp + lit;
-            const int32_t mlc = (int32_t)(tok & 15u);
-            const uint32_t pq = (uint32_t)(po < 28 ? po : 28);
-            const uint32_t dwo = lit <= 12 ? window_dword(wa, (uint32_t)po) : dword32(wa, wb, pq);
-            const uint32_t bsh = 8u * ((uint32_t)po - pq);
-            int32_t off = (int32_t)((dwo >> bsh) & 0xFFFFu);
-            const int32_t e0 = (int32_t)((dwo >> (bsh + 16)) & 0xFFu);
-            int32_t ml = mlc + (mlc == 15 ? e0 : 0);
-            const bool slow = (po + 3 > 32) | ((mlc == 15) & (e0 == 255)) | ((po + 3 > 16) & !wbok);
-            if (slow && act && !esc) {   // a long match length or the offset past the bytes at hand
-                const uint8_t* q = s + ipI;
-                off = (int32_t)q[po] | ((int32_t)q[po + 1] << 8);
-                ml = mlc;
-                if (ml == 15) {
-                    int32_t pe = po + 2;
-                    uint32_t b;
-                    do {
-                        b = q[pe];
-                        ++pe;
-                        ml += (int32_t)b;
-                    } while (b == 255 && pe < iend - ipI);
-                }
-                wait_vm0();   // (so no later use waits for these loads)
-            }
-            ml += 4;
-            const int32_t len = act && !esc ? lit + ml : 0;
-            int32_t tot;
-            const int32_t o = oF + quad_excl_sum(len, t, tot);
-            // the history base the round runs with: never below the base of
-            // the round decoded before it, never past F - 16 (what it drops
-            // is flushed, and far sources are final in HBM now)
-            const int32_t bq = oF - bD > kQH - kQRoom ? max(bD, min(oF - kQKeep, F - 16) & ~15) : bD;
-            const bool ok = act && !esc && o + lit + ml <= bq + kQH;
-            const uint32_t nb = (uint32_t)(__ballot(!ok) >> (lane & 60)) & 0xFu;
-            const int32_t use = nb ? __builtin_ctz(nb) : 4;
-            const bool u = t < use;
-            const int32_t s0 = o + lit - off;
-            const bool far = u & (s0 < bq) & (s0 >= 0);
-            const bool far1 = far & (ml > 16) & (s0 + 16 < bq);
-            // unconditional requests (lanes without a far source read the dummy slot)
-#ifdef LZ4M_QUAD_NOFAR   // A/B timing only (wrong bytes): far sources not requested
-            Rd.g0 = ld16(dmy);
-            Rd.g1 = ld16(dmy);
-#else
-            Rd.g0 = ld16(far ? d + s0 : dmy);
-            Rd.g1 = ld16(far1 ? d + s0 + 16 : dmy);
-#endif
-            const uint32_t sh = (uint32_t)lp;
-            Rd.x0 = u32x4{__builtin_amdgcn_alignbyte(wa.y, wa.x, sh), __builtin_amdgcn_alignbyte(wa.z, wa.y, sh),
-                          __builtin_amdgcn_alignbyte(wa.w, wa.z, sh), __builtin_amdgcn_alignbyte(wb.x, wa.w, sh)};
-            const int32_t outU = qsel(o - oF, use, tot);   // output of the used sequences
-            const int32_t ipU = qsel(ipI, use, ipF);       // input position after them
-            Rd.v = vI;
-            Rd.k = kI;
-            Rd.use = use;
-            Rd.lit = lit;
-            Rd.off = off;
-            Rd.ml = ml;
-            Rd.o = o;
-            Rd.ip = ipI;
-            Rd.lp = lp;
-            Rd.b = bq;
-            Rd.oEnd = oF + outU;
-            Rd.fl = (far ? kQFar : 0u) | (far1 ? kQFar1 : 0u) |
-                    ((u & (lp + lit > 16) & ((lp + lit > 32) | !wbok)) ? kQLitHbm : 0u);
-            if (vI) {
-                vI = false;
-                bD = bq;
-                if (use == 4) {
-                    oF += tot;
-                } else if (use > 0) {   // restart the stages behind it at the first unused sequence
-                    oF += outU;
-                    kF = kI + use;
-                    ipF = ipU;
-                    vL = false;
-                } else {   // the big path (3a) runs it and restarts the stages
-                    wait_big = true;
-                    vL = false;
-                }
-            }
-            QPIN4(Rd.x0);
-            QPIN(Rd.lit, Rd.off, Rd.ml, Rd.o);
-            QPIN(Rd.ip, Rd.lp, Rd.b, Rd.oEnd);
-            QPIN(Rd.use, Rd.k, (int32_t)Rd.fl, oF);
-            QPIN(kF, ipF, (int32_t)Rd.v, (int32_t)wait_big);
-        }
-        RP_MARK(12);
-        // ---- 2b. stage L into stage I: place the round's sequences, request their inputs
-        {
-            const bool lv = vL && kL + t < nseq;
-            const uint32_t lsh = 8u * (uint32_t)((uintptr_t)(dl + kL + t) & 3u);
-            const int32_t lenL = (int32_t)((lenX >> lsh) & 0xFFu);
-            int32_t tot;
-            const int32_t ex = quad_excl_sum(lv ? lenL : 0, t, tot);
-            const int32_t ipn = ipF + ex;
-            if (vL) {
-                ipI = ipn;
-                ip0I = ipF;
-                ipF += tot;
-                kI = kL;
-                lenI = lv ? lenL : 0;
-                vI = true;
-                vL = false;
-            }
-            QPIN(ipI, ipF, kI, lenI);
-            // the quad's 128-byte window at the round's first sequence (lane t:
-            // bytes 16t and 64 + 16t: contiguous per quad); near the block's
-            // end each lane's own 32 bytes at ipI clamped into the block (good
-            // sequences: ipI + 16 < iend); stages without a round read the
-            // dummy slot
-            const bool wm = ip0I + 128 <= iend;
-            const uint8_t* ia = !vI ? dmy : wm ? s + ip0I + 16 * t : s + (ipI + 16 <= iend ? ipI : 0);
-            const uint8_t* ib = !vI ? dmy : wm ? s + ip0I + 64 + 16 * t : s + (ipI + 32 <= iend ? ipI + 16 : iend - 16);
-            na = ld16(ia);
-            nb = ld16(ib);
-        }
-        RP_MARK(13);
-        // ---- 2c. request the next round's length bytes
-        {
-            const bool go = have && !wait_big && kF < nseq;
-            const int32_t k = kF + t;
-            // the aligned dword holding the byte (never past the scratch
-            // end; masked where it is used)
-            const uint8_t* lq = go ? dl + (k < nseq ? k : nseq - 1) : dmy;
-            lenY = *(const uint32_t*)(lq - ((uintptr_t)lq & 3u));   // (pointer arithmetic: stays a global access)
-            // touch: lanes 0-1 the input 256 bytes ahead, lanes 2-3 the lengths 64 ahead
-            const int32_t ti = min(ipF + 256, iend - 4), tl = min(kF + 64, nseq - 4);
-            const uint8_t* tq = !have ? dmy : t < 2 ? s + (ti > 0 ? ti : 0) : dl + (tl > 0 ? tl : 0);
-            tY = *(const uint32_t*)(tq - ((uintptr_t)tq & 3u));
-            if (go) {
-                kL = kF;
-                kF += 4;
-                vL = true;
-            }
-        }
-        asm volatile("" ::: "memory");
-        RP_MARK(14);
-        // ---- 3. execute Rx
-        // 3a. a sequence that does not fit the history (or is longer than the
-        // parse records): flush, copy it in HBM with the whole wave, reload
-        // the history.  The parse verified it: every read stays in the block.
-        uint64_t bigq = __ballot(Rx.v && Rx.use == 0 && t == 0);
-        RP_COUNT(18, __popcll(bigq));
-        if (bigq != 0) {
-            do {
-                const int q = __builtin_ctzll(bigq);
-                bigq &= bigq - 1;
-                lds_u8* const QB = (lds_u8*)(hists + (q >> 2) * kQHS);
-                const uint8_t* const sq = readlane_ptr(s, q);
-                uint8_t* const dq = readlane_ptr(d, q);
-                const int32_t qip = __builtin_amdgcn_readlane(Rx.ip, q), qo = __builtin_amdgcn_readlane(Rx.o, q);
-                const int32_t qF = __builtin_amdgcn_readlane(F, q), qb = __builtin_amdgcn_readlane(base, q);
-                const int32_t qiend = __builtin_amdgcn_readlane(iend, q);
-                for (int32_t c = qF + 16 * lane; c < qo; c += 1024) gbl_put(dq + c, lds_ld16(QB + (c - qb)), qo - c);
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-                const uint32_t tk = sq[qip];
-                int32_t L = (int32_t)(tk >> 4), p = qip + 1;
-                if (L == 15) {
-                    uint32_t b;
-                    do {
-                        b = sq[p];
-                        ++p;
-                        L += (int32_t)b;
-                    } while (b == 255 && p < qiend);
-                }
-                const int32_t ofs = (int32_t)sq[p + L] | ((int32_t)sq[p + L + 1] << 8);
-                int32_t pe = p + L + 2, M = (int32_t)(tk & 15u);
-                if (M == 15) {
-                    uint32_t b;
-                    do {
-                        b = sq[pe];
-                        ++pe;
-                        M += (int32_t)b;
-                    } while (b == 255 && pe < qiend);
-                }
-                M += 4;
-                wave_copy_literal(dq + qo, sq + p, L, lane);
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-                wave_copy_match(dq + qo + L, ofs, M, lane);
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-                const int32_t on = qo + L + M;
-                const int32_t nb = (on > kQKeep ? on - kQKeep : 0) & ~15;
-                // on < oend - 64: the 16-byte reads stay inside the block's slot
-                for (int32_t c = nb + 16 * lane; c < on; c += 1024) lds_st16(QB + (c - nb), ld16(dq + c));
-                if ((lane >> 2) == (q >> 2)) {
-                    base = bD = nb;
-                    F = on & ~15;   // [F, on) is in HBM already; rewriting it later is harmless
-                    kF = Rx.k + 1;
-                    ipF = pe;
-                    oF = on;
-                    wait_big = false;
-                    Rx.v = false;
-                    if (kF >= nseq) have = false;   // the block's good prefix is done
-                }
-            } while (bigq != 0);
-            wait_vm0();
-        }
-        RP_MARK(9);
-        RP_COUNT(17, __popcll(__ballot(Rx.v && t == 0)));
-        RP_COUNT(21, __popcll(__ballot(Rx.v && t < Rx.use)));
-        // 3b. rebase to the round's base: the kept bytes move to the front
-        // (one quad at a time, with the whole wave)
-        uint64_t rq = __ballot(Rx.v && Rx.b != base && t == 0);
-        RP_COUNT(19, __popcll(rq));
-        while (rq != 0) {
-            const int q = __builtin_ctzll(rq);
-            rq &= rq - 1;
-            lds_u8* const QB = (lds_u8*)(hists + (q >> 2) * kQHS);
-            const int32_t qb = __builtin_amdgcn_readlane(base, q), qn = __builtin_amdgcn_readlane(Rx.b, q);
-            const int32_t qo = __builtin_amdgcn_readlane(Rx.o, q);   // the round's first output position
-            // moving down: a step's reads precede its writes, and its writes
-            // stay below the next step's reads
-            for (int32_t c0 = 0; c0 < qo - qn; c0 += 1024) {
-                const bool cp = c0 + 16 * lane < qo - qn;
-                const u32x4 v = lds_ld16(QB + (cp ? qn - qb + c0 + 16 * lane : 0));
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-                if (cp) lds_st16(QB + c0 + 16 * lane, v);
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-            }
-        }
-        if (Rx.v) base = Rx.b;
-        RP_MARK(10);
-        // 3c. the round, in order: one lane of each quad per sub-step
-        // (exec-masked: an LDS access costs per active lane)
-        {
-            const bool u = Rx.v && t < Rx.use;
-            const int32_t litE = Rx.lit, offE = Rx.off, mlE = Rx.ml, oE = Rx.o;
-            const int32_t m = oE + litE, s0 = m - offE;
-            const bool far = (Rx.fl & kQFar) != 0, far1 = (Rx.fl & kQFar1) != 0;
-            const bool per = offE < 16;
-            const int32_t stp = per ? 16 - (16 % (offE > 0 ? offE : 1)) : 16;   // the second chunk's offset
-            const bool c2 = mlE > stp;                                          // a second chunk
-            const bool n2 = c2 && !per && !far1 && offE >= 32;                  // its source, read with the first's
-            lds_u8* const aL = HB + (oE - base);
-            lds_u8* const aM = HB + (m - base);
-            lds_u8* const aS = HB + (far ? 0 : s0 - base);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                if (u && t == j) {
-                    lds_st16(aL, Rx.x0);   // literal (wild)
-                    if (litE > 16) {       // (rare) bytes 16.. from HBM (inside the block: good)
-                        for (int32_t i = 16; i < litE; i += 16) lds_st16(aL + i, ld16(s + Rx.ip + Rx.lp + i));
-                        wait_vm0();
-                    }
-                    u32x4 v1 = lds_ld16(aS);
-                    u32x4 v2 = lds_ld16(HB + (n2 ? s0 + 16 - base : 0));   // (s0 + 16 >= base when n2)
-                    v1 = far ? Rx.g0 : v1;
-                    if (per) v1 = period_pattern(v1, (uint32_t)(offE > 0 ? offE : 1));   // s0 >= base: never far
-                    lds_st16(aM, v1);   // match, first chunk (wild)
-                    if (c2) {
-                        if (per) {
-                            for (int32_t i = stp; i < mlE; i += stp) lds_st16(aM + i, v1);
-                        } else {
-                            if (!n2 && !far1) v2 = lds_ld16(HB + (s0 + 16 - base));   // its source overlaps chunk 1
-                            lds_st16(aM + 16, far1 ? Rx.g1 : v2);
-                            if (mlE > 32) {   // (rare) the rest of a long match
-                                for (int32_t i = 32; i < mlE; i += 16) {
-                                    const int32_t sp = s0 + i;   // sp < base: flushed when the round was decoded
-                                    if (sp >= base) {
-                                        lds_st16(aM + i, lds_ld16(HB + (sp - base)));
-                                    } else {
-                                        lds_st16(aM + i, ld16(d + sp));
-                                        wait_vm0();
-                                    }
-                                }
-                            }
-                        }
-                    }
-                }
-                // the sub-steps run in lane order: without this the compiler
-                // may merge the four identical conditional blocks into one
-                // (in C++ each lane runs its block once either way)
-                asm volatile("" ::: "memory");
-            }
-        }
-        RP_MARK(11);
-        // 3d. flush up to 64 finished bytes (16 per lane; lanes with nothing
-        // final store to their dummy slot)
-        {
-            const int32_t c = F + 16 * t;
-            const bool fl = Rx.v && c + 16 <= Rx.oEnd;
-            const u32x4 v = lds_ld16(HB + (fl ? c - base : 0));
-            if (fl) st16(d + c, v);
-            const int32_t nf = (Rx.oEnd - F) >> 4;
-            if (Rx.v) F += 16 * (nf < 4 ? nf : 4);
-            if (__any(Rx.v && Rx.oEnd - F >= 64)) {   // behind after a long round: 64 more
-                const int32_t c2 = F + 16 * t;
-                const bool f2 = Rx.v && c2 + 16 <= Rx.oEnd;
-                const u32x4 v2 = lds_ld16(HB + (f2 ? c2 - base : 0));
-                if (f2) st16(d + c2, v2);
-                const int32_t n2 = (Rx.oEnd - F) >> 4;
-                if (Rx.v) F += 16 * (n2 < 4 ? n2 : 4);
-            }
-            if (Rx.v && Rx.k + Rx.use >= nseq) {   // the block's good prefix is done: flush the rest exactly
-                for (int32_t cc = F + 16 * t; cc < Rx.oEnd; cc += 64) gbl_put(d + cc, lds_ld16(HB + (cc - base)), Rx.oEnd - cc);
-                have = false;
-            }
-            Rx.v = false;
-        }
-        junk += tX;   // (the touch of the iteration before: long arrived)
-        asm volatile("" ::: "memory");
-        return ++guard >= max_iters;
-    };
-    while (!step(R0, R1, waA, wbA, waB, wbB, lenA, lenB, tA, tB) &&
-           !step(R1, R0, waB, wbB, waA, wbA, lenB, lenA, tB, tA)) {
-    }
-    if (junk == 0x9E3779B9u && n < 0) dummy[0] = 0;   // (keeps the touches; never true: n >= 0)
-    RP_FLUSH(8, 32);
-    if (dbg != nullptr && guard >= max_iters) {   // diagnostic builds: the state of a wave that hit the bound
-        int32_t* o = dbg + (size_t)(blockIdx.x % 64) * 64 * 16 + lane * 16;
-        o[0] = (int32_t)have | ((int32_t)done << 1) | ((int32_t)wait_big << 2) | ((int32_t)vL << 3) |
-               ((int32_t)vI << 4) | ((int32_t)R0.v << 5) | ((int32_t)R1.v << 6);
-        o[1] = nseq; o[2] = kF; o[3] = ipF; o[4] = oF; o[5] = base; o[6] = F; o[7] = kL;
-        o[8] = kI; o[9] = bD; o[10] = 0; o[11] = iend; o[12] = 0; o[13] = lenI; o[14] = (int32_t)blockIdx.x;
-        o[15] = 0x5A5A;
-    }
-}
-
 }  // namespace lz4m
 
 using namespace lz4m;
@@ -1603,51 +1061,35 @@ extern "C" int lz4m_rows_prof(unsigned long long* out, int reset) {
 }
 #endif
 
-// diagnostics (tools/debug_quad.py): an iteration bound for quad_exec_kernel
-// and a buffer for the state of waves that reach it
-static uint32_t g_quad_max_iters = 1u << 30;
-static int32_t* g_quad_dbg = nullptr;
-extern "C" void lz4m_quad_debug(int32_t* dbg, uint32_t max_iters) {
-    g_quad_dbg = dbg;
-    g_quad_max_iters = max_iters ? max_iters : (1u << 30);
-}
-
 extern "C" size_t lz4m_rows_fixed_bytes(int64_t n) { return kRowsMeta + (size_t)n * sizeof(RowMeta); }
 
 extern "C" int lz4m_rows_launch(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len,
                                 uint8_t* d_dst, const int64_t* d_dst_off, const int32_t* d_dst_cap, int64_t n,
-                                void* d_work, size_t work_bytes, int parse_grid, int exec_grid, int quad, hipStream_t stream) {
+                                void* d_work, size_t work_bytes, int parse_grid, int exec_grid, hipStream_t stream) {
     const size_t fixed = lz4m_rows_fixed_bytes(n);
     if (work_bytes < fixed) return LZ4M_ROWS_ENOSPACE;
     unsigned long long* ctr = static_cast<unsigned long long*>(d_work);
     RowMeta* meta = reinterpret_cast<RowMeta*>(static_cast<uint8_t*>(d_work) + kRowsMeta);
-    uint8_t* dummy = static_cast<uint8_t*>(d_work) + kRowsDummy;
     uint8_t* lens = static_cast<uint8_t*>(d_work) + fixed;
     const int64_t lens_cap = (int64_t)(work_bytes - fixed);
     hipError_t e = hipMemsetAsync(ctr, 0, 64, stream);
     if (e != hipSuccess) return (int)e;
     hipLaunchKernelGGL(rows_parse_kernel, dim3((uint32_t)parse_grid), dim3(kPWG), 0, stream, d_src, d_src_off,
                        d_src_len, d_dst_cap, n, meta, lens, lens_cap, ctr);
-    if (quad)
-        hipLaunchKernelGGL(quad_exec_kernel, dim3((uint32_t)exec_grid), dim3(64), 0, stream, d_src, d_src_off,
-                           d_src_len, d_dst, d_dst_off, meta, lens, n, ctr, dummy, g_quad_max_iters, g_quad_dbg);
-    else
-        hipLaunchKernelGGL(rows_exec_kernel, dim3((uint32_t)exec_grid), dim3(64), 0, stream, d_src, d_src_off,
-                           d_src_len, d_dst, d_dst_off, meta, lens, n, ctr);
+    hipLaunchKernelGGL(rows_exec_kernel, dim3((uint32_t)exec_grid), dim3(64), 0, stream, d_src, d_src_off, d_src_len,
+                       d_dst, d_dst_off, meta, lens, n, ctr);
     return (int)hipGetLastError();
 }
 
-extern "C" int lz4m_rows_grids(int64_t n, int quad, int* parse_grid, int* exec_grid) {
+extern "C" int lz4m_rows_grids(int64_t n, int* parse_grid, int* exec_grid) {
     int dev = 0, cus = 0, pk = 0, ek = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&pk, reinterpret_cast<const void*>(rows_parse_kernel), kPWG, 0);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &ek, quad ? reinterpret_cast<const void*>(quad_exec_kernel) : reinterpret_cast<const void*>(rows_exec_kernel), 64,
-        0);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&ek, reinterpret_cast<const void*>(rows_exec_kernel), 64, 0);
     if (cus <= 0) cus = 256;
     const int64_t ps = (int64_t)cus * (pk > 0 ? pk : 1), es = (int64_t)cus * (ek > 0 ? ek : 1);
-    const int64_t pneed = (n + kPWG - 1) / kPWG, eneed = quad ? (n + 15) / 16 : (n + 3) / 4;
+    const int64_t pneed = (n + kPWG - 1) / kPWG, eneed = (n + 3) / 4;
     *parse_grid = (int)(pneed < ps ? pneed : ps);
     *exec_grid = (int)(eneed < es ? eneed : es);
     return 0;
