@@ -112,6 +112,9 @@ __device__ __forceinline__ u32x4 period_pattern(u32x4 w, uint32_t off) {
 // 4 bytes -- replays at ~56 cycles per wave-instruction on gfx950
 // (tools/micro/lds_align.hip; cdna_hip_programming.md Guideline 17), and the
 // decoders' history buffers are read and written at arbitrary byte offsets.
+#ifndef LZ4M_LDS_SKIP
+#define LZ4M_LDS_SKIP 0    // A/B: the last two masked ORs of a put only where some lane needs them
+#endif
 #ifndef LZ4M_LDS_ALIGN
 #define LZ4M_LDS_ALIGN 1   // 0 = plain (unaligned) wide accesses; 2 = plain stores for wholly covered dwords
 #endif
@@ -178,6 +181,14 @@ __device__ __forceinline__ void lds_put_al(lds_u8* p, u32x4 v, int32_t k, lds_cu
     if (m.y == ~0u) { *(vu32*)(q + 4) = d1; } else if (m.y) { LZ4M_MSKOR(b4, 4, m.y, d1); }
     if (m.z == ~0u) { *(vu32*)(q + 8) = d2; } else if (m.z) { LZ4M_MSKOR(b4, 8, m.z, d2); }
     if (m.w == ~0u) { *(vu32*)(q + 12) = d3; } else if (m.w) { LZ4M_MSKOR(b4, 12, m.w, d3); }
+    if (m4) LZ4M_MSKOR(b4, 16, m4, d4);
+#elif LZ4M_LDS_SKIP
+    // dwords 3 and 4 hold bytes only for puts reaching past byte 12 of the
+    // span (kk > 12 - r): skipped where no lane of the wave needs them
+    LZ4M_MSKOR(b4, 0, m.x, d0);
+    LZ4M_MSKOR(b4, 4, m.y, d1);
+    LZ4M_MSKOR(b4, 8, m.z, d2);
+    if (m.w) LZ4M_MSKOR(b4, 12, m.w, d3);
     if (m4) LZ4M_MSKOR(b4, 16, m4, d4);
 #else
     LZ4M_MSKOR(b4, 0, m.x, d0);

@@ -276,6 +276,14 @@ constexpr int kPWG = LZ4M_PARSE_WG;     // parse workgroup (LDS is allocated per
 #ifndef LZ4M_PARSE_PAIR
 #define LZ4M_PARSE_PAIR 0               // A/B: two sequences per fast step (measured -1.5 %)
 #endif
+#ifndef LZ4M_PARSE_COOP
+#define LZ4M_PARSE_COOP 1               // A/B: ring refills loaded by four lanes per block (64-byte requests)
+#endif
+// a 64-bit address received from another lane, as a global pointer
+__device__ __forceinline__ const uint8_t* readlane_safe_ptr(uint64_t a) {
+    typedef __attribute__((address_space(1))) const uint8_t gu8;
+    return (const uint8_t*)(gu8*)(uintptr_t)a;
+}
 #ifndef LZ4M_PARSE_MIN_ACTIVE
 #define LZ4M_PARSE_MIN_ACTIVE 40        // run the general step once fewer lanes than this can go on
 #endif
@@ -379,11 +387,36 @@ __global__ __launch_bounds__(kPWG) void rows_parse_kernel(const uint8_t* __restr
         RP_COUNT(6, __popcll(__ballot(live && need)));
         // ---- the general step
         // rotate requested bytes in (every lane past the first half of its ring)
+#if LZ4M_PARSE_COOP
+        {
+            // block b's 64 requested bytes are held by lanes 4 (b % 16) ..
+            // + 3, 16 bytes each, in pf[b / 16]
+            const uint64_t R = __ballot(live && pfv && ip >= wb + 64);
+            if (R) {
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const int bb = 16 * c + (int)(lane >> 2);
+                    const int32_t wbb = __builtin_amdgcn_ds_bpermute(bb << 2, wb);
+                    if ((R >> bb) & 1ull) {
+                        lds_u8* Wb = (lds_u8*)(wins + bb * kPWS);
+                        const int32_t h = (wbb >> 6) & 1;
+                        lds_st16(Wb + 64 * h + 16 * (int32_t)(lane & 3), pf[c]);
+                        if (h == 0 && (lane & 3) == 0) lds_st16(Wb + kPW, pf[c]);
+                    }
+                }
+                if ((R >> lane) & 1ull) {
+                    wb += 64;
+                    pfv = false;
+                }
+            }
+        }
+#else
         if (live && pfv && ip >= wb + 64) {
             ring_put(W, (wb >> 6) & 1, pf);
             wb += 64;
             pfv = false;
         }
+#endif
         if (live && need) {
             need = false;
             if (ip + 32 > wb + kPW) {   // no bytes ahead (block start, a long literal): load the ring now
@@ -462,10 +495,34 @@ __global__ __launch_bounds__(kPWG) void rows_parse_kernel(const uint8_t* __restr
             kf += kPStage / 2;
         }
         // request the next 64 bytes ahead
+#if LZ4M_PARSE_COOP
+        {
+            // four lanes per block, 16 contiguous bytes each: one 64-byte
+            // request per block instead of four 16-byte ones
+            const uint64_t Q = __ballot(live && !pfv && wb + kPW < iend);
+            if (Q) {
+                const uint64_t na = (uint64_t)(uintptr_t)(s + wb + kPW);
+                const int32_t left = iend - (wb + kPW);
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const int bb = 16 * c + (int)(lane >> 2);
+                    const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(bb << 2, (int32_t)(uint32_t)na);
+                    const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(bb << 2, (int32_t)(uint32_t)(na >> 32));
+                    const int32_t lf = __builtin_amdgcn_ds_bpermute(bb << 2, left) - 16 * (int32_t)(lane & 3);
+                    if ((Q >> bb) & 1ull) {
+                        const uint8_t* q = readlane_safe_ptr(((uint64_t)hi << 32) | lo) + 16 * (lane & 3);
+                        pf[c] = lf >= 16 ? ld16(q) : ld16_guarded(q, lf);
+                    }
+                }
+                if ((Q >> lane) & 1ull) pfv = true;
+            }
+        }
+#else
         if (live && !pfv && wb + kPW < iend) {
             load64(s, wb + kPW, iend, pf);
             pfv = true;
         }
+#endif
         // ---- the common sequence, straight-line, until too few lanes can go on
         RP_MARK(1);
         const int32_t thr = min(LZ4M_PARSE_MIN_ACTIVE, (int)__popcll(__ballot(live)));
