@@ -874,7 +874,6 @@ __global__ __launch_bounds__(256, 4) void hist_decompress_kernel(const uint8_t* 
             // speculative parse + walk: lane k gets the k-th sequence start
             int32_t myseq = 0;
             int nseq = 0;
-            bool stop = false;
             int32_t pos = ip - ib;
             // The chain of starts by pointer jumping instead of a serial readlane
             // walk.  Each lane parses two positions (pos + lane, pos + 64 + lane);
@@ -917,10 +916,7 @@ __global__ __launch_bounds__(256, 4) void hist_decompress_kernel(const uint8_t* 
                 }
                 const int32_t cv = __builtin_amdgcn_readlane(c, nn);   // the first start not taken
                 nseq = nn;
-                if (cv < 128) {   // a non-simple sequence
-                    stop = true;
-                    break;
-                }
+                if (cv < 128) break;   // a non-simple sequence
                 pos += cv;
             }
             HP_MARK(1);

@@ -35,6 +35,7 @@
 #include <limits.h>
 
 namespace lz4m {
+typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
 
 // LZ4M_ROWS_PROF (diagnostic builds only, tools/prof_rows.sh): per-phase
 // wave-cycle sums and event counts of the two kernels, read with lz4m_rows_prof.
@@ -596,7 +597,7 @@ __global__ __launch_bounds__(kPWG) void rows_parse_kernel(const uint8_t* __restr
 // the 32 bytes of the NEXT round are requested while this round copies, so a
 // round waits on at most one memory round trip (its far match sources).
 #ifndef LZ4M_ROWS_H
-#define LZ4M_ROWS_H 2048
+#define LZ4M_ROWS_H 1024   // history per row (bytes): 1 KiB measured as fast as 2 KiB at equal occupancy
 #endif
 constexpr int32_t kRowsH = LZ4M_ROWS_H;
 #ifndef LZ4M_ROWS_LITPUT
@@ -660,14 +661,18 @@ __device__ __forceinline__ u32x4 period_perm(u32x4 w, lds_cu32* sel) {
     return r;
 }
 
-// One round of a row, parsed: lane jj's sequence (start t, literal at t + lp,
-// lit / off / ml), its output position o, the round's row totals, the
-// literal's first 32 bytes and the far sources requested from HBM.
+// One round of a row, parsed: lane jj's sequence (literal at input position
+// t, lit / off / ml), its output position o, the round's row totals and the
+// far source requested from HBM; the literal's first 32 bytes go to XS.
+// The literal's first 32 bytes go to the lane's LDS slot (two 16-byte
+// aligned entries), not to registers: a parsed round waits there while the
+// previous one executes, and the registers it frees hold the executor at 5
+// waves per SIMD (1 KiB histories).
 struct PSeq {
-    u32x4 x0, x1, pre0, pre1;
-    int32_t t, lp, lit, off, ml, o, dlt;
-    int32_t use, opn, ipn;   // uniform across the row
-    uint32_t fl;
+    u32x4 pre0;                       // the far source's first 16 bytes, requested
+    int32_t t, lit, off, ml, o, dlt;  // t: the literal's input position
+    int32_t opn, ipn;                 // uniform across the row
+    uint32_t fl;                      // flags | (use << 8): the row takes its first `use` lanes
 };
 constexpr uint32_t kFlU = 1, kFlFar = 2, kFlLate = 4, kFlLitHbm = 8;
 
@@ -678,7 +683,7 @@ constexpr uint32_t kFlU = 1, kFlFar = 2, kFlLate = 4, kFlLitHbm = 8;
 // below F (flushed), else marked late (requested once flushed).
 __device__ __forceinline__ void parse_round(PSeq& P, int32_t jj, int32_t r, int32_t k0, int32_t nseq, int32_t ip,
                                             int32_t op, int32_t bnext, int32_t F, const uint8_t* s, const uint8_t* d,
-                                            int32_t iend, int32_t dlt, int32_t t, u32x4 wa, u32x4 wb) {
+                                            int32_t iend, int32_t dlt, int32_t t, u32x4 wa, u32x4 wb, lds_u32x4* XS) {
     const bool act = k0 + jj < nseq;
     const bool esc = dlt == 255;   // length >= 255: the parse left it to be re-parsed
     const bool wbok = t + 32 <= iend;
@@ -724,28 +729,33 @@ __device__ __forceinline__ void parse_round(PSeq& P, int32_t jj, int32_t r, int3
     const bool u = jj < use;
     P.opn = op + row_last(row_incl_sum(u ? len : 0));
     P.ipn = ip + row_last(row_incl_sum(u ? dlt : 0));
-    P.use = use;
     const int32_t s0 = o + lit - off;
     const bool far = u & (s0 < bnext);
     const bool late = far & (s0 + 32 > F);
     const bool pf = far & !late;
     // unconditional requests (lanes without a far source read the block start)
     P.pre0 = ld16(d + (pf ? s0 : 0));
-    P.pre1 = ld16(d + ((pf & (ml > 16)) ? s0 + 16 : 0));
     const uint32_t sh = (uint32_t)lp;
-    P.x0 = u32x4{__builtin_amdgcn_alignbyte(wa.y, wa.x, sh), __builtin_amdgcn_alignbyte(wa.z, wa.y, sh),
+    XS[0] = u32x4{__builtin_amdgcn_alignbyte(wa.y, wa.x, sh), __builtin_amdgcn_alignbyte(wa.z, wa.y, sh),
                  __builtin_amdgcn_alignbyte(wa.w, wa.z, sh), __builtin_amdgcn_alignbyte(wb.x, wa.w, sh)};
-    P.x1 = u32x4{__builtin_amdgcn_alignbyte(wb.y, wb.x, sh), __builtin_amdgcn_alignbyte(wb.z, wb.y, sh),
+    XS[1] = u32x4{__builtin_amdgcn_alignbyte(wb.y, wb.x, sh), __builtin_amdgcn_alignbyte(wb.z, wb.y, sh),
                  __builtin_amdgcn_alignbyte(wb.w, wb.z, sh), __builtin_amdgcn_alignbyte(0u, wb.w, sh)};
-    P.t = t;
-    P.lp = lp;
+    P.t = t + lp;
     P.lit = lit;
     P.off = off;
     P.ml = ml;
     P.o = o;
     P.dlt = dlt;
-    P.fl = (u ? kFlU : 0u) | (far ? kFlFar : 0u) | (late ? kFlLate : 0u) |
+    P.fl = ((uint32_t)use << 8) | (u ? kFlU : 0u) | (far ? kFlFar : 0u) | (late ? kFlLate : 0u) |
            ((u & (lp + lit > 16) & ((lp + lit > 32) | !wbok)) ? kFlLitHbm : 0u);
+}
+
+// 16 * jj recomputed where it is used on the rare paths (block end, a
+// sequence that does not fit): kept live across the loop it was spilled
+__device__ __forceinline__ int32_t cold_j16(int32_t jj) {
+    int32_t v = 16 * jj;
+    asm volatile("" : "+v"(v));
+    return v;
 }
 
 // history base a row runs its next round with, given the output position op
@@ -778,7 +788,7 @@ __device__ __forceinline__ int32_t load_len(const uint8_t* dl, int32_t k, int32_
 // (its far sources in flight) and round R + 2's inputs are requested, so a
 // round waits on no memory latency of its own.
 #ifndef LZ4M_ROWS_WAVES
-#define LZ4M_ROWS_WAVES 4   // waves per SIMD the executor's registers are held to (LDS allows 4)
+#define LZ4M_ROWS_WAVES 5   // waves per SIMD the executor's registers are held to (LDS allows 5)
 #endif
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LZ4M_ROWS_WAVES, 8))) void rows_exec_kernel(const uint8_t* __restrict__ src,
                                                        const int64_t* __restrict__ src_off,
@@ -794,6 +804,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LZ4M_ROWS_WA
     __shared__ __attribute__((aligned(16))) uint8_t dums[64 * 16];
 #endif
     __shared__ __attribute__((aligned(16))) uint32_t psel[16 * 8];
+    __shared__ __attribute__((aligned(16))) u32x4 xsl[64 * 2];
     const uint32_t lane = threadIdx.x;
     const int32_t jj = (int32_t)(lane & 15), r = (int32_t)(lane >> 4);
     lds_u8* HB = (lds_u8*)(hists + r * kRowsHS);
@@ -815,6 +826,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LZ4M_ROWS_WA
         psel[e] = v;
     }
     lds_cu32* PS = (lds_cu32*)psel;
+    lds_u32x4* XSL = (lds_u32x4*)(xsl + 2 * lane);
     // this lane's dummy store target (flush stores of lanes with nothing final)
     uint8_t* const dst_dummy = reinterpret_cast<uint8_t*>(ctr) + kRowsDummy + 1024 * (blockIdx.x % kRowsDummySlots) + 16 * lane;
     (void)dst_dummy;
@@ -826,7 +838,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LZ4M_ROWS_WA
     bool have = false, sync = true;
     PSeq P, Q;   // P: the round to execute; Q: the next one, parsed ahead
     // inputs of the round after Q: start tn, bytes na|nb, length dn; dnn = the one after
-    int32_t tn = 0, dn = 0, dnn = 0;
+    int32_t dn = 0, dnn = 0;
     u32x4 na = u32x4{0, 0, 0, 0}, nb = na;
     RP_DECL
     while (true) {
@@ -864,20 +876,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LZ4M_ROWS_WA
             const int32_t tc = ip + row_incl_sum(dc) - dc;
             u32x4 wa, wb;
             load_in(s, tc, iend, wa, wb);
-            parse_round(P, jj, r, k0, nseq, ip, op, base, F, s, d, iend, dc, tc, wa, wb);
+            parse_round(P, jj, r, k0, nseq, ip, op, base, F, s, d, iend, dc, tc, wa, wb, XSL);
             dn = load_len(dl, k0 + 16 + jj, nseq);
-            tn = P.ipn + row_incl_sum(dn) - dn;
-            load_in(s, tn, iend, na, nb);
+            load_in(s, P.ipn + row_incl_sum(dn) - dn, iend, na, nb);
             dnn = load_len(dl, k0 + 32 + jj, nseq);
             sync = false;
 #if LZ4M_ROWS_COUNTED
             wait_vm0();   // (rare: block starts, short rounds) the common path's waits stay counted
 #endif
         }
-        if (P.use == 0) {
+        if ((P.fl >> 8) == 0) {
             sync = true;
             if (k0 >= nseq) {   // the block's good prefix is done: flush the rest exactly
-                for (int32_t c = F + 16 * jj; c < op; c += 256) gbl_put(d + c, lds_ld16(HB + (c - base)), op - c);
+                for (int32_t c = F + cold_j16(jj); c < op; c += 256) gbl_put(d + c, lds_ld16(HB + (c - base)), op - c);
                 have = false;
 #if LZ4M_ROWS_COUNTED
                 wait_vm0();
@@ -909,7 +920,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LZ4M_ROWS_WA
                 } while (b == 255 && qe < iend);
             }
             M += 4;
-            for (int32_t c = F + 16 * jj; c < op; c += 256) gbl_put(d + c, lds_ld16(HB + (c - base)), op - c);
+            for (int32_t c = F + cold_j16(jj); c < op; c += 256) gbl_put(d + c, lds_ld16(HB + (c - base)), op - c);
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
             row_copy_literal(d + op, s + q, L, jj);
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
@@ -920,7 +931,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LZ4M_ROWS_WA
             k0 += 1;
             base = (op > kRowsKeep ? op - kRowsKeep : 0) & ~15;
             // op < oend - 64: the 16-byte reads stay inside the block's slot
-            for (int32_t c = base + 16 * jj; c < op; c += 256) lds_st16(HB + (c - base), ld16(d + c));
+            for (int32_t c = base + cold_j16(jj); c < op; c += 256) lds_st16(HB + (c - base), ld16(d + c));
             F = op;
 #if LZ4M_ROWS_COUNTED
             wait_vm0();
@@ -932,15 +943,38 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LZ4M_ROWS_WA
         RP_MARK(10);
         RP_COUNT(16, 1);
         RP_COUNT(18, __popcll(__ballot((P.fl & kFlU) != 0)));
+        {
+        const bool u = (P.fl & kFlU) != 0;
+        const int32_t lit = P.lit, o = P.o;
+        // literals: bytes lp.. of the input (exact, branch-free); longer ones rare
+#if LZ4M_LDS_ALIGN
+        if (u && lit > 0) lds_put_al(HB + (o - base), XSL[0], lit, MT);
+#elif LZ4M_ROWS_LITPUT == 1
+        if (u && lit > 0) lds_put_bf(HB + (o - base), DUM, XSL[0], lit);
+#elif LZ4M_ROWS_LITPUT == 2
+        if (u && lit > 0) lds_put_masked(HB + (o - base), XSL[0], lit);
+#else
+        lds_put_bf(HB + (o - base), DUM, XSL[0], u ? lit : 0);
+#endif
+        if (u && lit > 16) {
+            if (!(P.fl & kFlLitHbm)) {
+                LDS_PUT(HB + (o - base + 16), XSL[1], lit - 16);
+            } else {   // a literal beyond the bytes at hand: from HBM (inside the block: good)
+                for (int32_t i = 16; i < lit; i += 16) LDS_PUT(HB + (o - base + i), ld16(s + P.t + i), lit - i);
+#if LZ4M_ROWS_COUNTED
+                wait_vm0();
+#endif
+            }
+        }
+        }
         // ---- parse the next round ahead (its far sources are requested now),
         // then request the inputs of the round after it
-        const bool ahead = P.use == 16 && k0 + 16 < nseq;
+        const bool ahead = (P.fl >> 8) == 16 && k0 + 16 < nseq;
         if (ahead) {
             const int32_t bq = next_base(P.opn, base);
-            parse_round(Q, jj, r, k0 + 16, nseq, P.ipn, P.opn, bq, F, s, d, iend, dn, tn, na, nb);
+            parse_round(Q, jj, r, k0 + 16, nseq, P.ipn, P.opn, bq, F, s, d, iend, dn, P.ipn + row_incl_sum(dn) - dn, na, nb, XSL);
             dn = dnn;
-            tn = Q.ipn + row_incl_sum(dn) - dn;
-            load_in(s, tn, iend, na, nb);
+            load_in(s, Q.ipn + row_incl_sum(dn) - dn, iend, na, nb);
             dnn = load_len(dl, k0 + 48 + jj, nseq);
         }
         RP_MARK(11);
@@ -948,26 +982,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LZ4M_ROWS_WA
         const bool u = (P.fl & kFlU) != 0;
         const int32_t lit = P.lit, off = P.off, ml = P.ml, o = P.o;
         const int32_t m = o + lit, mend = m + ml, s0 = m - off;
-        // literals: bytes lp.. of the input (exact, branch-free); longer ones rare
-#if LZ4M_LDS_ALIGN
-        if (u && lit > 0) lds_put_al(HB + (o - base), P.x0, lit, MT);
-#elif LZ4M_ROWS_LITPUT == 1
-        if (u && lit > 0) lds_put_bf(HB + (o - base), DUM, P.x0, lit);
-#elif LZ4M_ROWS_LITPUT == 2
-        if (u && lit > 0) lds_put_masked(HB + (o - base), P.x0, lit);
-#else
-        lds_put_bf(HB + (o - base), DUM, P.x0, u ? lit : 0);
-#endif
-        if (u && lit > 16) {
-            if (!(P.fl & kFlLitHbm)) {
-                LDS_PUT(HB + (o - base + 16), P.x1, lit - 16);
-            } else {   // a literal beyond the bytes at hand: from HBM (inside the block: good)
-                for (int32_t i = 16; i < lit; i += 16) LDS_PUT(HB + (o - base + i), ld16(s + P.t + P.lp + i), lit - i);
-#if LZ4M_ROWS_COUNTED
-                wait_vm0();
-#endif
-            }
-        }
         RP_MARK(12);
         // readiness passes: a match is copied once no earlier pending match of
         // the round writes into its source [s0, se)
@@ -997,7 +1011,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LZ4M_ROWS_WA
                     if (!per) {
                         const int32_t sp = s0 + i;
                         // sp < base: flushed (F >= base + kRowsKeep - 16)
-                        v = (far && !late && i == 16) ? P.pre1 : sp >= base ? lds_ld16u(HB + (sp - base)) : ld16(d + sp);
+                        v = sp >= base ? lds_ld16u(HB + (sp - base)) : ld16(d + sp);
                     }
                     LDS_PUT(HB + (m - base + i), v, ml - i);
                 }
@@ -1047,7 +1061,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LZ4M_ROWS_WA
                     } else {
                         const int32_t sp = s0 + i;
                         // sp < base: flushed (F >= base + kRowsKeep - 16)
-                        v = (far && !late && i == 16) ? P.pre1 : sp >= base ? lds_ld16u(HB + (sp - base)) : ld16(d + sp);
+                        v = sp >= base ? lds_ld16u(HB + (sp - base)) : ld16(d + sp);
                     }
                     lds_put(HB + (m - base + i), v, ml - i);
                 }
@@ -1079,7 +1093,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LZ4M_ROWS_WA
         F += (opn - F) & ~15;
         op = opn;
         ip = P.ipn;
-        k0 += P.use;
+        k0 += (int32_t)(P.fl >> 8);
         const int32_t nbse = next_base(op, base);
         if (nbse != base) {
             // the kept bytes lie >= kRowsH - kRowsRoom - kRowsKeep past the
