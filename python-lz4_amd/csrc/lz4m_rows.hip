@@ -264,7 +264,28 @@ __device__ __forceinline__ uint32_t dword32(u32x4 a, u32x4 b, uint32_t k) {
 // parse.  Recorded lengths are staged in a 64-entry LDS ring per lane and
 // leave for HBM 32 at a time.
 constexpr int kPW = 128;                // ring bytes
-constexpr int kPWS = kPW + 16;          // ring + mirror
+#ifndef LZ4M_PARSE_NOMIRROR
+#define LZ4M_PARSE_NOMIRROR 1           // 16-byte ring reads wrap per aligned 8-byte piece (no mirror: 16 waves/CU, -0.9 ms)
+#endif
+constexpr int kPWS = LZ4M_PARSE_NOMIRROR ? kPW : kPW + 16;   // ring (+ mirror)
+// 16 ring bytes at ring offset x (0..kPW-1)
+__device__ __forceinline__ u32x4 ring_ld16(const lds_u8* W, int32_t x) {
+#if LZ4M_PARSE_NOMIRROR
+    // three aligned 8-byte reads, each wrapped into the ring, and a funnel shift
+    const uint32_t a = (uint32_t)x & ~7u;
+    const uint64_t x0 = *(const lds_vu64*)(W + a), x1 = *(const lds_vu64*)(W + ((a + 8u) & (kPW - 1))),
+                   x2 = *(const lds_vu64*)(W + ((a + 16u) & (kPW - 1)));
+    const bool h = (x & 4) != 0;
+    const uint32_t r = (uint32_t)x & 3u;
+    const uint32_t c0 = (uint32_t)x0, c1 = (uint32_t)(x0 >> 32), c2 = (uint32_t)x1, c3 = (uint32_t)(x1 >> 32),
+                   c4 = (uint32_t)x2, c5 = (uint32_t)(x2 >> 32);
+    const uint32_t e0 = h ? c1 : c0, e1 = h ? c2 : c1, e2 = h ? c3 : c2, e3 = h ? c4 : c3, e4 = h ? c5 : c4;
+    return u32x4{__builtin_amdgcn_alignbyte(e1, e0, r), __builtin_amdgcn_alignbyte(e2, e1, r),
+                 __builtin_amdgcn_alignbyte(e3, e2, r), __builtin_amdgcn_alignbyte(e4, e3, r)};
+#else
+    return lds_ld16u(W + x);
+#endif
+}
 #ifndef LZ4M_PARSE_STAGE
 #define LZ4M_PARSE_STAGE 32
 #endif
@@ -293,7 +314,7 @@ __device__ __forceinline__ const uint8_t* readlane_safe_ptr(uint64_t a) {
 __device__ __forceinline__ void ring_put(lds_u8* W, int32_t h, const u32x4* v) {
 #pragma unroll
     for (int c = 0; c < 4; ++c) lds_st16(W + 64 * h + 16 * c, v[c]);
-    if (h == 0) lds_st16(W + kPW, v[0]);
+    if (!LZ4M_PARSE_NOMIRROR && h == 0) lds_st16(W + kPW, v[0]);
 }
 
 __device__ __forceinline__ void load64(const uint8_t* s, int32_t x, int32_t iend, u32x4* v) {
@@ -402,7 +423,7 @@ __global__ __launch_bounds__(kPWG) void rows_parse_kernel(const uint8_t* __restr
                         lds_u8* Wb = (lds_u8*)(wins + bb * kPWS);
                         const int32_t h = (wbb >> 6) & 1;
                         lds_st16(Wb + 64 * h + 16 * (int32_t)(lane & 3), pf[c]);
-                        if (h == 0 && (lane & 3) == 0) lds_st16(Wb + kPW, pf[c]);
+                        if (!LZ4M_PARSE_NOMIRROR && h == 0 && (lane & 3) == 0) lds_st16(Wb + kPW, pf[c]);
                     }
                 }
                 if ((R >> lane) & 1ull) {
@@ -535,9 +556,9 @@ __global__ __launch_bounds__(kPWG) void rows_parse_kernel(const uint8_t* __restr
             if (go) {
                 // straight-line: no short-circuit tests
                 const bool inw = ip + 16 <= wb + kPW;
-                const u32x4 w = lds_ld16u(W + (ip & (kPW - 1)));
+                const u32x4 w = ring_ld16(W, ip & (kPW - 1));
 #if LZ4M_PARSE_PAIR
-                const u32x4 w2 = lds_ld16u(W + ((ip + 16) & (kPW - 1)));   // the next 16 ring bytes
+                const u32x4 w2 = ring_ld16(W, (ip + 16) & (kPW - 1));   // the next 16 ring bytes
 #endif
                 const int32_t tok = (int32_t)(w.x & 0xFFu), lit = tok >> 4, mlc = tok & 15;
                 const bool mlx = mlc == 15;
@@ -613,8 +634,15 @@ constexpr int32_t kRowsH = LZ4M_ROWS_H;
 #define LZ4M_ROWS_COUNTED 0   // A/B: a fixed number of memory operations per round on the common path (measured -1 %)
 #endif
 constexpr int32_t kRowsHS = kRowsH + 32;   // buffer stride (16-byte reads past the end stay inside)
-constexpr int32_t kRowsKeep = kRowsH / 2;   // history kept on a rebase
-constexpr int32_t kRowsRoom = 512;          // rebase when less room than this is left
+#ifndef LZ4M_ROWS_KEEP
+#define LZ4M_ROWS_KEEP (kRowsH / 2)
+#endif
+#ifndef LZ4M_ROWS_ROOM
+#define LZ4M_ROWS_ROOM 512
+#endif
+constexpr int32_t kRowsKeep = LZ4M_ROWS_KEEP;   // history kept on a rebase
+constexpr int32_t kRowsRoom = LZ4M_ROWS_ROOM;   // rebase when less room than this is left
+static_assert(kRowsKeep % 16 == 0 && kRowsKeep + kRowsRoom <= kRowsH, "history split");
 
 // Row-cooperative exact copies in HBM (16 lanes, lane j = jj).
 __device__ __forceinline__ void row_copy_literal(uint8_t* d, const uint8_t* s, int32_t len, int32_t jj) {

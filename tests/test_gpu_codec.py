@@ -200,7 +200,10 @@ def test_decompress_dict(gpu, oracle, corpus):
 
 def test_xxh32_batch(gpu, oracle, corpus):
     blocks, ragged = corpus
-    items = blocks[:32] + ragged
+    # lengths around the lane loop's 8-stripe prefetch groups (128 / 256 B)
+    edge = [blocks[0][:k] for k in (0, 1, 15, 16, 17, 127, 128, 129, 255, 256, 257, 271, 272, 383, 384, 385,
+                                   511, 512, 4095, 34567)]
+    items = blocks[:32] + ragged + edge
     packed, offs, lens = _pack(items)
     d = N.to_device(packed, gpu)
     out = torch.empty(len(items), dtype=torch.int32, device=gpu)

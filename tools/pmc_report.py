@@ -3,10 +3,10 @@
 One decoder launch = the row decoder's three kernels (parse, execution,
 finisher); the k-th dispatch of each kernel belongs to launch k.  Launch
 order in `bench.py --steps 1 --warmup 0 --no-compress`: launch 0 is the
-silesia-like headline launch (config 2); the next two are the random-data
-launches (warmup + step), whose bytes are known (pure streaming: read ~=
-compressed size, write = decoded size) and serve as the calibration of the
-request counters.  The summary carries the hash of the decoder sources
+silesia-like headline launch (config 2), then the 65 536-block mid-batch
+launches, and the LAST launch is a random-data launch, whose bytes are known
+(pure streaming: read ~= compressed size, write = decoded size) and serves as
+a check of the method on the decoder itself.  The summary carries the hash of the decoder sources
 (bench.decoder_src_sha) so bench.py reports roofline.traffic only for the
 kernels that were profiled."""
 import collections
@@ -51,7 +51,7 @@ def hbm_bytes_reqsize(c):
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 if len(sys.argv) > 2:
-    head, rand = out[0], out.get(1)
+    head, rand = out[0], (out[max(out)] if len(out) > 1 else None)
     rd, wr = hbm_bytes(head)
     summary = {
         "kernel": "+".join(KERNELS),
