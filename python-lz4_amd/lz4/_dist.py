@@ -152,14 +152,22 @@ class _Null:
 
 def _page_bounds(lens: torch.Tensor, page_blocks: int) -> torch.Tensor:
     """Byte offsets of the page cuts of one shard: page k = blocks
-    [k * page_blocks, (k + 1) * page_blocks); returns int64 [pages + 1]."""
+    [k * page_blocks, (k + 1) * page_blocks); returns int64 [pages + 1].
+    Per-page sums (a plain reduction) and a scan over the few page sums: a
+    device-wide scan of every block length is a look-back scan whose waiting
+    workgroups would sit on CUs beside the next wave's compression."""
     n = lens.numel()
-    csum = torch.zeros(n + 1, dtype=torch.int64, device=lens.device)
-    if n:
-        torch.cumsum(lens.to(torch.int64), 0, out=csum[1:])
     pages = (n + page_blocks - 1) // page_blocks
-    idx = (torch.arange(pages + 1, device=lens.device) * page_blocks).clamp_(max=n)
-    return csum[idx]
+    out = torch.zeros(pages + 1, dtype=torch.int64, device=lens.device)
+    if n:
+        full = n // page_blocks
+        sums = torch.zeros(pages, dtype=torch.int64, device=lens.device)
+        if full:
+            sums[:full] = lens[: full * page_blocks].view(full, page_blocks).to(torch.int64).sum(1)
+        if n > full * page_blocks:
+            sums[full] = lens[full * page_blocks:].to(torch.int64).sum()
+        torch.cumsum(sums, 0, out=out[1:])
+    return out
 
 
 def compress_gather_waves(compress_wave, waves: int, root: int = 0, group=None, overlap: bool = True,
