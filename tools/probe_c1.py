@@ -21,3 +21,23 @@ for rep in range(2):
     td = (time.perf_counter() - t) / len(blocks)
 assert back == blocks
 print(f"per call: compress {tc * 1e6:.1f} us, decompress {td * 1e6:.1f} us")
+
+# fixed per-call cost: the same entry points on (almost) no work -- a 1-byte
+# empty block (cap 0) and a 64 KiB run of zeros (one long match: 64 KiB back
+# over PCIe, little kernel work); compress of 16 zero bytes
+import ctypes as C  # noqa: E402
+import lz4._native as N  # noqa: E402
+lib = N.lib()
+z = bytes(65536)
+cz = B.compress(z, store_size=False)
+out = C.create_string_buffer(65536 + 64)
+cases = {"decompress empty (cap 0)": lambda: lib.lz4m_decompress_safe(b"\x00", out, 1, 0),
+         "decompress 64 KiB zeros": lambda: lib.lz4m_decompress_safe(cz, out, len(cz), 65536),
+         "compress 16 zero bytes": lambda: lib.lz4m_compress_default(bytes(16), out, 16, 64)}
+for name, f in cases.items():
+    for _ in range(20):
+        f()
+    t = time.perf_counter()
+    for _ in range(500):
+        f()
+    print(f"{name}: {(time.perf_counter() - t) / 500 * 1e6:.1f} us per call")
