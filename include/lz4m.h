@@ -231,6 +231,39 @@ int lz4m_compress_batch(const uint8_t* d_src, const int64_t* d_src_off, const in
                         lz4m_stream_t stream);
 
 /*
+ * lz4m_decompress_solo: lz4m_decompress_batch_ws for ONE block whose input is
+ * at most 66 KiB - 64 bytes (src_len_host, the same value as d_src_len[0]),
+ * with the compressed block staged in LDS first (the lone decode then waits
+ * on no input round trip).  Same bytes and status as the batched decoders
+ * (LZ4_decompress_safe, lz4.c:2436-2441); used by lz4m_decompress_safe.
+ * The input, its record (d_src_off .. d_dst_cap) and d_status may live in
+ * mapped pinned host memory (hipHostMalloc; the device's address of it); the
+ * output d_dst must be device memory.  h_out: nullptr, or a mapped pinned
+ * host buffer that also receives the decoded bytes at the end of the launch.
+ * h_done: nullptr, or a mapped pinned host int the launch sets to 1 with a
+ * system-scope release once the status and h_out are in host memory (a
+ * caller may poll it instead of synchronising the stream).
+ */
+int lz4m_decompress_solo(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len,
+                         uint8_t* d_dst, const int64_t* d_dst_off, const int32_t* d_dst_cap,
+                         int32_t* d_status, int32_t src_len_host, uint8_t* h_out, int32_t* h_done,
+                         lz4m_stream_t stream);
+
+/*
+ * lz4m_compress_solo: lz4m_compress_batch for ONE block of len < 65547 bytes
+ * (table U16_HASH4, U32_HASH5 or AUTO), with the block staged in LDS so the
+ * latency-bound lone parse reads no source byte from memory.  Same bytes as
+ * the batched kernel; used by the single-call host functions below
+ * (lz4m_compress_default / lz4m_compress_block_api).  LZ4M_EINVAL when len is
+ * out of range.  d_src and d_out_len may live in mapped pinned host memory;
+ * d_dst must be device memory; h_out: nullptr, or a mapped pinned host
+ * buffer that also receives the compressed bytes at the end of the launch;
+ * h_done: as for lz4m_decompress_solo.
+ */
+int lz4m_compress_solo(const uint8_t* d_src, int32_t len, uint8_t* d_dst, int32_t cap, int32_t* d_out_len,
+                       int table, int acceleration, uint8_t* h_out, int32_t* h_done, lz4m_stream_t stream);
+
+/*
  * Batched one-shot XXH32 (xxhash.c:392-416): d_out[i] = XXH32(block i, seed).
  * Replaces the per-block checksum calls of lz4frame.c:846 (block checksum)
  * and lz4frame.c:1819 (its verification).

@@ -687,6 +687,75 @@ __global__ __launch_bounds__(64) void compress_kernel(const uint8_t* __restrict_
     }
 }
 
+// One lone block of < 65547 bytes (the single-call API, lz4m_host.hip): the
+// workgroup's four waves stage the whole block in LDS, then wave 0 runs the
+// same parse with every source read -- hash inputs, candidates, catch-up,
+// match extension, literals -- from LDS instead of L2/HBM.  A lone block is
+// latency-bound (the skip-ahead search waits one memory round trip per 64
+// attempts); occupancy does not matter for a batch of one, so 64 KiB of LDS
+// per workgroup is free here.  Output bytes are the batched kernel's.
+constexpr int kSoloMax = kLimit64K - 1;                  // the U16 table's range (lz4.c:1352)
+constexpr int kSoloBuf = ((kSoloMax + 64) + 15) & ~15;   // + zero padding past the block
+constexpr int kSoloU = 4;   // 16-byte pieces in flight per lane when staging / copying out
+template <int V, bool ACC1>
+__global__ __launch_bounds__(256) void compress_solo_kernel(const uint8_t* __restrict__ src, int32_t len,
+                                                            uint8_t* dst, int32_t cap, int32_t* __restrict__ out_len,
+                                                            int accel, uint8_t* h_out, int32_t* h_done) {
+    __shared__ int32_t solo_r;
+    __shared__ __attribute__((aligned(16))) uint8_t blk[kSoloBuf];
+    __shared__ __attribute__((aligned(16))) uint16_t tab[8192];
+    RING_DECL
+    const uint32_t t = threadIdx.x;
+    constexpr int kStep = 16 * 256;
+    const int32_t lim = len + 64 < kSoloBuf ? len + 64 : kSoloBuf;   // the block and 64 zero bytes
+    for (int32_t base = 0; base < lim; base += kSoloU * kStep) {   // four pieces in flight per lane (16 measured no faster over PCIe)
+        u32x4 v[kSoloU];
+#pragma unroll
+        for (int u = 0; u < kSoloU; ++u) {
+            const int32_t p = base + u * kStep + 16 * (int32_t)t;
+            v[u] = p + 16 <= len ? ld16(src + p) : ld16_guarded(src + p, len - p);
+        }
+#pragma unroll
+        for (int u = 0; u < kSoloU; ++u) {
+            const int32_t p = base + u * kStep + 16 * (int32_t)t;
+            if (p < lim) lds_st16((lds_u8*)blk + p, v[u]);
+        }
+    }
+    __syncthreads();
+    if (t < kWave) {
+        const int64_t r = compress_block<V, ACC1>((const uint8_t*)blk, len, dst, cap, accel, tab, ring, t);
+        if (t == 0) {
+            *out_len = (int32_t)r;
+            solo_r = (int32_t)r;
+        }
+    }
+    // the compressed bytes to the caller's mapped host buffer, all four waves,
+    // so the call needs no device-to-host copy of its own
+    __syncthreads();
+    const int32_t r = solo_r;
+    for (int32_t base = 0; h_out != nullptr && base < r; base += kSoloU * kStep) {
+        u32x4 v[kSoloU];
+#pragma unroll
+        for (int u = 0; u < kSoloU; ++u) {
+            const int32_t p = base + u * kStep + 16 * (int32_t)t;
+            v[u] = p + 16 <= r ? ld16(dst + p) : ld16_guarded(dst + p, r - p);
+        }
+#pragma unroll
+        for (int u = 0; u < kSoloU; ++u) {
+            const int32_t p = base + u * kStep + 16 * (int32_t)t;
+            if (p + 16 <= r) {
+                st16(h_out + p, v[u]);
+            } else {
+                for (int32_t k = p; k < r; ++k) h_out[k] = dst[k];
+            }
+        }
+    }
+    if (h_done != nullptr) {   // all of the above visible to the host, then the flag it polls
+        __syncthreads();
+        if (t == 0) __hip_atomic_store(h_done, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Blocks with history: lz4.block.compress(dict=) and linked frames.
 // ---------------------------------------------------------------------------
@@ -883,6 +952,36 @@ using namespace lz4m;
 extern "C" int lz4m_compress_bound(int input_size) {
     if ((unsigned)input_size > (unsigned)kMaxInput) return 0;
     return input_size + input_size / 255 + 16;
+}
+
+extern "C" int lz4m_compress_solo(const uint8_t* d_src, int32_t len, uint8_t* d_dst, int32_t cap,
+                                  int32_t* d_out_len, int table, int acceleration, uint8_t* h_out,
+                                  int32_t* h_done, lz4m_stream_t stream) {
+    if (len < 0 || len > kSoloMax || cap < 0) return LZ4M_EINVAL;
+    if (acceleration < 1) acceleration = 1;        // lz4.c:1350-1351
+    if (acceleration > 65537) acceleration = 65537;
+    hipStream_t s = (hipStream_t)stream;
+    auto go = [&](auto v_tag) {
+        constexpr int V = decltype(v_tag)::value;
+        if (acceleration == 1)
+            hipLaunchKernelGGL((compress_solo_kernel<V, true>), dim3(1), dim3(256), 0, s, d_src, len, d_dst, cap,
+                               d_out_len, acceleration, h_out, h_done);
+        else
+            hipLaunchKernelGGL((compress_solo_kernel<V, false>), dim3(1), dim3(256), 0, s, d_src, len, d_dst, cap,
+                               d_out_len, acceleration, h_out, h_done);
+    };
+    switch (table) {
+        case LZ4M_TABLE_AUTO:       // len < 65547: the byU16 parse (lz4.c:1352-1357)
+        case LZ4M_TABLE_U16_HASH4:
+            go(std::integral_constant<int, LZ4M_TABLE_U16_HASH4>{});
+            break;
+        case LZ4M_TABLE_U32_HASH5:
+            go(std::integral_constant<int, LZ4M_TABLE_U32_HASH5>{});
+            break;
+        default:
+            return LZ4M_EINVAL;
+    }
+    return (int)hipGetLastError();
 }
 
 extern "C" int lz4m_compress_batch(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len,

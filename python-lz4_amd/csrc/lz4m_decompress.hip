@@ -811,14 +811,23 @@ __device__ unsigned long long g_hist_prof[16];
 // whole source lies in the dictionary takes the parallel path (its bytes are
 // read from there); anything else that reaches before the block goes to the
 // exact state machine with the same dictionary (decode_step<true>).
-template <bool DICT>
+// SOLO (lz4m_decompress_solo, the single-call API: n == 1, input <=
+// kSoloIn bytes): the workgroup first stages the whole compressed block in
+// LDS, and every input read -- the speculative parse windows, length runs,
+// long literals, the exact state machine -- is an LDS read.  A lone block is
+// latency-bound (a stored-looking 64 KiB block waits on ~40 dependent memory
+// round trips); the batch instances are unchanged.
+constexpr int32_t kSoloIn = 66 * 1024;   // > LZ4_compressBound(65536) + 64
+constexpr int kSoloU = 4;               // 16-byte pieces in flight per lane when staging / copying out
+template <bool DICT, bool SOLO = false>
 __global__ __launch_bounds__(256, 4) void hist_decompress_kernel(const uint8_t* __restrict__ src,
                                                                  const int64_t* __restrict__ src_off,
                                                                  const int32_t* __restrict__ src_len, uint8_t* dst,
                                                                  const int64_t* __restrict__ dst_off,
                                                                  const int32_t* __restrict__ dst_cap,
                                                                  int32_t* __restrict__ status, int64_t n,
-                                                                 const int32_t* __restrict__ dict_len, int64_t ddelta) {
+                                                                 const int32_t* __restrict__ dict_len, int64_t ddelta,
+                                                                 uint8_t* solo_out, int32_t* solo_done) {
     __shared__ __attribute__((aligned(16))) uint8_t ins[4][kCoopIn + 64];
     __shared__ __attribute__((aligned(16))) uint8_t outs[4][kHistW + 32];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -836,12 +845,38 @@ __global__ __launch_bounds__(256, 4) void hist_decompress_kernel(const uint8_t* 
 #define HLD(p) lds_ld16(p)
 #endif
     HP_DECL
+    const uint8_t* solo_src = nullptr;
+    __shared__ int32_t solo_r;
+    if constexpr (SOLO) {
+        __shared__ __attribute__((aligned(16))) uint8_t sblk[kSoloIn];
+        const uint8_t* g = src + src_off[0];
+        const int32_t len = src_len[0];   // <= kSoloIn - 64 (host-checked); zeros past it
+        constexpr int32_t kStep = 16 * 256;
+        const int32_t lim = len + 64 < kSoloIn ? len + 64 : kSoloIn;   // the block and 64 zero bytes
+        for (int32_t base0 = 0; base0 < lim; base0 += kSoloU * kStep) {   // four pieces in flight per lane (16 measured no faster over PCIe)
+            u32x4 v[kSoloU];
+#pragma unroll
+            for (int u = 0; u < kSoloU; ++u) {
+                const int32_t p = base0 + u * kStep + 16 * (int32_t)threadIdx.x;
+                v[u] = p + 16 <= len ? ld16(g + p) : ld16_guarded(g + p, len - p);
+            }
+#pragma unroll
+            for (int u = 0; u < kSoloU; ++u) {
+                const int32_t p = base0 + u * kStep + 16 * (int32_t)threadIdx.x;
+                if (p < lim) lds_st16((lds_u8*)sblk + p, v[u]);
+            }
+        }
+        __syncthreads();
+        solo_src = (const uint8_t*)sblk;
+    }
     for (int64_t b = (int64_t)blockIdx.x * 4 + wv; b < n; b += (int64_t)gridDim.x * 4) {
-        const uint8_t* s = src + src_off[b];
+        const uint8_t* s = SOLO ? solo_src : src + src_off[b];
         uint8_t* d = dst + dst_off[b];
         const int32_t iend = src_len[b], oend = dst_cap[b];
         if (oend < 0 || iend <= 0 || oend == 0) {   // lz4.c:1950, :1978-1983
-            if (lane == 0) status[b] = (oend == 0 && iend == 1 && s[0] == 0) ? 0 : -1;
+            const int32_t r0 = (oend == 0 && iend == 1 && s[0] == 0) ? 0 : -1;
+            if (lane == 0) status[b] = r0;
+            if (SOLO && lane == 0) solo_r = r0;
             continue;
         }
         const bool fast = oend >= 64;
@@ -1055,8 +1090,41 @@ __global__ __launch_bounds__(256, 4) void hist_decompress_kernel(const uint8_t* 
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
         const int32_t r = coop_finish<DICT>(s, d, iend, oend, ip, op, fast, lane, dlen, d + ddelta);
         if (lane == 0) status[b] = r;
+        if (SOLO && lane == 0) solo_r = r;
         HP_MARK(7);
         HP_COUNT(11, 1);
+    }
+    if constexpr (SOLO) {
+        // the decoded bytes to the caller's mapped host buffer, all four waves
+        // (wave 0 decoded; the others skipped the loop), so the call needs no
+        // device-to-host copy of its own
+        __syncthreads();
+        const int32_t r = solo_r;
+        if (solo_out != nullptr && r > 0) {
+            const uint8_t* d0 = dst + dst_off[0];
+            constexpr int32_t kStep = 16 * 256;
+            for (int32_t base0 = 0; base0 < r; base0 += kSoloU * kStep) {
+                u32x4 v[kSoloU];
+#pragma unroll
+                for (int u = 0; u < kSoloU; ++u) {
+                    const int32_t p = base0 + u * kStep + 16 * (int32_t)threadIdx.x;
+                    v[u] = p + 16 <= r ? ld16(d0 + p) : ld16_guarded(d0 + p, r - p);
+                }
+#pragma unroll
+                for (int u = 0; u < kSoloU; ++u) {
+                    const int32_t p = base0 + u * kStep + 16 * (int32_t)threadIdx.x;
+                    if (p + 16 <= r) {
+                        st16(solo_out + p, v[u]);
+                    } else if (p < r) {
+                        put_exact(solo_out + p, v[u], (uint32_t)(r - p));
+                    }
+                }
+            }
+        }
+        if (solo_done != nullptr) {   // all of the above visible to the host, then the flag it polls
+            __syncthreads();
+            if (threadIdx.x == 0) __hip_atomic_store(solo_done, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
     HP_FLUSH();
 #undef HPUT
@@ -1220,7 +1288,17 @@ extern "C" int lz4m_decompress_batch_sel(const uint8_t* d_src, const int64_t* d_
     }
     const int64_t grid = (n + 3) / 4;
     hipLaunchKernelGGL(hist_decompress_kernel<false>, dim3((uint32_t)(grid < 65536 ? grid : 65536)), dim3(256), 0, st,
-                       d_src, d_src_off, d_src_len, d_dst, d_dst_off, d_dst_cap, d_status, n, nullptr, (int64_t)0);
+                       d_src, d_src_off, d_src_len, d_dst, d_dst_off, d_dst_cap, d_status, n, nullptr, (int64_t)0, nullptr, nullptr);
+    return (int)hipGetLastError();
+}
+
+extern "C" int lz4m_decompress_solo(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len,
+                                    uint8_t* d_dst, const int64_t* d_dst_off, const int32_t* d_dst_cap,
+                                    int32_t* d_status, int32_t src_len_host, uint8_t* h_out, int32_t* h_done,
+                                    lz4m_stream_t stream) {
+    if (src_len_host < 0 || src_len_host > kSoloIn - 64) return LZ4M_EINVAL;
+    hipLaunchKernelGGL((hist_decompress_kernel<false, true>), dim3(1), dim3(256), 0, (hipStream_t)stream, d_src,
+                       d_src_off, d_src_len, d_dst, d_dst_off, d_dst_cap, d_status, (int64_t)1, nullptr, (int64_t)0, h_out, h_done);
     return (int)hipGetLastError();
 }
 
@@ -1241,7 +1319,7 @@ extern "C" int lz4m_decompress_batch(const uint8_t* d_src, const int64_t* d_src_
     const int64_t grid = (n + 3) / 4;
     hipLaunchKernelGGL(hist_decompress_kernel<false>, dim3((uint32_t)(grid < 65536 ? grid : 65536)), dim3(256), 0,
                        (hipStream_t)stream, d_src, d_src_off, d_src_len, d_dst, d_dst_off, d_dst_cap, d_status, n,
-                       nullptr, (int64_t)0);
+                       nullptr, (int64_t)0, nullptr, nullptr);
     return (int)hipGetLastError();
 }
 
@@ -1269,7 +1347,7 @@ extern "C" int lz4m_decompress_batch_prefix(const uint8_t* d_src, const int64_t*
     const int64_t delta = (int64_t)((intptr_t)d_dict_base - (intptr_t)d_dst);
     hipLaunchKernelGGL(hist_decompress_kernel<true>, dim3((uint32_t)(grid < 65536 ? grid : 65536)), dim3(256), 0,
                        (hipStream_t)stream, d_src, d_src_off, d_src_len, d_dst, d_dst_off, d_dst_cap, d_status, n,
-                       d_dict_len, delta);
+                       d_dict_len, delta, nullptr, nullptr);
     return (int)hipGetLastError();
 }
 

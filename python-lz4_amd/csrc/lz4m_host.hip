@@ -16,6 +16,8 @@ namespace {
 
 constexpr int kMaxInput = 0x7E000000;   // LZ4_MAX_INPUT_SIZE, lz4.h:211
 constexpr size_t kMeta = 256;           // per-call record (offsets, sizes, result, decoder scratch)
+constexpr int kSoloLimit = 65536 + 11;  // LZ4_64Klimit (lz4.c:689): lz4m_compress_solo's range
+constexpr int kSoloDecIn = 66 * 1024 - 64;   // lz4m_decompress_solo's input range
 
 // Per-thread device buffer, pinned host staging buffer and stream, for the
 // device that is current when the call is made.  A call is then one
@@ -25,13 +27,14 @@ struct Scratch {
     int dev = -1;
     uint8_t* buf = nullptr;
     uint8_t* host = nullptr;
+    uint8_t* host_dev = nullptr;   // the device's address of `host` (mapped pinned memory)
     size_t cap = 0;
     hipStream_t stream = nullptr;
     void release() {
         if (buf) (void)hipFree(buf);
         if (host) (void)hipHostFree(host);
         if (stream) (void)hipStreamDestroy(stream);
-        buf = host = nullptr;
+        buf = host = host_dev = nullptr;
         stream = nullptr;
         cap = 0;
     }
@@ -47,11 +50,12 @@ struct Scratch {
         if (bytes > cap) {
             if (buf) (void)hipFree(buf);
             if (host) (void)hipHostFree(host);
-            buf = host = nullptr;
+            buf = host = host_dev = nullptr;
             cap = 0;
             const size_t want = bytes + bytes / 4 + 4096;
             if (hipMalloc(reinterpret_cast<void**>(&buf), want) != hipSuccess) return false;
             if (hipHostMalloc(reinterpret_cast<void**>(&host), want, hipHostMallocDefault) != hipSuccess) return false;
+            if (hipHostGetDevicePointer(reinterpret_cast<void**>(&host_dev), host, 0) != hipSuccess) return false;
             cap = want;
         }
         return true;
@@ -64,7 +68,7 @@ inline size_t up(size_t x) { return (x + 255) & ~(size_t)255; }
 
 struct CMeta {
     int64_t src_off, dst_off;
-    int32_t src_len, dst_cap, result, pad;
+    int32_t src_len, dst_cap, result, done;   // done: set by a lone-block kernel when its output is in host memory
     uint64_t work[8];   // decoder scratch (lz4m_decompress_workspace_bytes)
 };
 static_assert(sizeof(CMeta) <= kMeta, "record size");
@@ -99,10 +103,60 @@ int32_t one_block(const char* src, int32_t len, char* dst, int32_t cap, int32_t 
     return m.result;
 }
 
+// One block through a lone-block kernel (lz4m_compress_solo /
+// lz4m_decompress_solo) that reads its input and record straight from the
+// mapped pinned staging buffer and writes its result and output back into it:
+// no copies on the stream, one launch and one synchronisation per call (the
+// copies of one_block cost ~10 us each in launch gaps at 64 KiB).  Layout of
+// the pinned buffer as in one_block; the device buffer holds the output.
+template <typename Launch>
+int32_t one_block_mapped(const char* src, int32_t len, char* dst, int32_t cap, int32_t fail, Launch launch) {
+    const size_t in = up((size_t)len + 16);
+    if (!t_scratch.get(in + kMeta + (size_t)cap + 16)) return fail;
+    uint8_t* h = t_scratch.host;
+    uint8_t* hd = t_scratch.host_dev;
+    if (len) memcpy(h, src, (size_t)len);
+    CMeta m{};
+    m.src_off = 0;
+    m.dst_off = 0;   // output at the device buffer's start
+    m.src_len = len;
+    m.dst_cap = cap;
+    m.result = fail;
+    memcpy(h + in, &m, sizeof m);
+    hipStream_t s = t_scratch.stream;
+    CMeta* hm = reinterpret_cast<CMeta*>(h + in);
+    if (launch(hd, reinterpret_cast<CMeta*>(hd + in), t_scratch.buf, hd + in + kMeta, s) != 0) return fail;
+    // the kernel's last act is a system-scope release of `done` after its
+    // output: poll it (the completion signal and the waiting thread's wake-up
+    // cost ~10 us more); every 256 polls check the stream, so a failed launch
+    // ends the wait
+    for (uint32_t i = 1; __atomic_load_n(&hm->done, __ATOMIC_ACQUIRE) == 0; ++i) {
+        if ((i & 255) == 0) {
+            const hipError_t q = hipStreamQuery(s);
+            if (q == hipSuccess && __atomic_load_n(&hm->done, __ATOMIC_ACQUIRE) == 0) return fail;   // ended without the flag
+            if (q != hipSuccess && q != hipErrorNotReady) return fail;
+        }
+        __builtin_ia32_pause();
+    }
+    memcpy(&m, h + in, sizeof m);
+    if (m.result > 0 && m.result <= cap) memcpy(dst, h + in + kMeta, (size_t)m.result);
+    return m.result;
+}
+
 // one-block compress through the batched compressors; returns the compressed size or 0
 int compress_one(const char* src, char* dst, int srcSize, int dstCapacity, int table, int acceleration) {
     if (srcSize < 0 || srcSize > kMaxInput || dstCapacity < 0 || (srcSize > 0 && !src) || (dstCapacity > 0 && !dst))
         return 0;
+    // blocks below 65547 bytes: the LDS-staged lone-block kernel (the
+    // skip-ahead search then waits on no memory round trip), no copies
+    if (srcSize < kSoloLimit) {
+        const int32_t r = one_block_mapped(
+            src, srcSize, dst, dstCapacity, 0, [&](uint8_t* hd, CMeta* hm, uint8_t* d, uint8_t* hout, hipStream_t s) {
+                return lz4m_compress_solo(hd, srcSize, d, dstCapacity, &hm->result, table, acceleration, hout,
+                                          &hm->done, reinterpret_cast<lz4m_stream_t>(s));
+            });
+        return r > 0 ? r : 0;
+    }
     const int32_t r = one_block(src, srcSize, dst, dstCapacity, 0, [&](uint8_t* d, CMeta* dm, hipStream_t s) {
         return lz4m_compress_batch(d, &dm->src_off, &dm->src_len, d, &dm->dst_off, &dm->dst_cap, &dm->result, 1,
                                    table, acceleration, reinterpret_cast<lz4m_stream_t>(s));
@@ -115,6 +169,15 @@ int compress_one(const char* src, char* dst, int srcSize, int dstCapacity, int t
 extern "C" int lz4m_decompress_safe(const char* src, char* dst, int compressedSize, int dstCapacity) {
     if (compressedSize < 0 || dstCapacity < 0) return -1;
     if ((compressedSize > 0 && !src) || (dstCapacity > 0 && !dst)) return -1;
+    // inputs up to 66 KiB - 64 (any 64 KiB block): the LDS-staged lone-block
+    // decoder, no copies
+    if (compressedSize <= kSoloDecIn)
+        return one_block_mapped(src, compressedSize, dst, dstCapacity, -1,
+                                [&](uint8_t* hd, CMeta* hm, uint8_t* d, uint8_t* hout, hipStream_t s) {
+                                    return lz4m_decompress_solo(hd, &hm->src_off, &hm->src_len, d, &hm->dst_off,
+                                                                &hm->dst_cap, &hm->result, compressedSize, hout,
+                                                                &hm->done, reinterpret_cast<lz4m_stream_t>(s));
+                                });
     return one_block(src, compressedSize, dst, dstCapacity, -1, [&](uint8_t* d, CMeta* dm, hipStream_t s) {
         return lz4m_decompress_batch_ws(d, &dm->src_off, &dm->src_len, d, &dm->dst_off, &dm->dst_cap, &dm->result, 1,
                                         dm->work, sizeof dm->work, reinterpret_cast<lz4m_stream_t>(s));

@@ -73,9 +73,23 @@ def _mode_accel(mode, acceleration: int) -> int:
     raise ValueError(f"Invalid mode argument: {mode}. Must be one of: standard, fast, high_compression")
 
 
+_probe = b"lz4m"
+_BYTES_DATA = C.cast(C.c_char_p(_probe), C.c_void_p).value - id(_probe)   # measured, not assumed
+del _probe
+
+
 def _addr(view: memoryview):
-    """Address of a contiguous host buffer (read-only ones too), None if empty."""
-    return int(np.frombuffer(view, dtype=np.uint8).ctypes.data) if view.nbytes else None
+    """Address of a contiguous host buffer (read-only ones too), None if empty.
+    A whole bytes object (its data offset measured at import) or a writable
+    buffer takes a fast path; numpy's .ctypes (~2.6 us) serves the rest."""
+    if not view.nbytes:
+        return None
+    obj = view.obj
+    if type(obj) is bytes and view.nbytes == len(obj):
+        return id(obj) + _BYTES_DATA   # CPython: the bytes' data sits at a fixed offset in the object
+    if not view.readonly:
+        return C.addressof(C.c_char.from_buffer(view))
+    return int(np.frombuffer(view, dtype=np.uint8).ctypes.data)
 
 
 def _i64(vals, dev) -> torch.Tensor:
@@ -109,12 +123,12 @@ def compress(source, mode="default", store_size=True, acceleration=1, compressio
         if d.nbytes > INT_MAX:
             raise OverflowError("Dictionary too large for LZ4 API")
     accel = _mode_accel(mode, acceleration)
-    if d is None:   # one call: lz4m_compress_block_api (one copy in, one launch, one copy out)
-        N.device()
+    if d is None:   # one call: lz4m_compress_block_api (one launch on mapped pinned staging)
+        N.require_device()
         n = src.nbytes
         hdr = _HDR if store_size else 0
         out = bytearray(hdr + max(N.compress_bound(n), 1))
-        optr = C.addressof((C.c_char * len(out)).from_buffer(out))
+        optr = C.addressof(C.c_char.from_buffer(out))
         r = N.lib().lz4m_compress_block_api(_addr(src), optr + hdr, n, len(out) - hdr, accel)
         if r <= 0:
             raise LZ4BlockError("Compression failed")
@@ -151,7 +165,7 @@ def decompress(source, uncompressed_size=-1, return_bytearray=False, dict=None):
         if dview.nbytes > INT_MAX:
             raise OverflowError("Dictionary too large for LZ4 API")
     if dview is None or not dview.nbytes:   # one call: lz4m_decompress_safe
-        N.device()
+        N.require_device()
         if uncompressed_size >= 0:
             cap, skip = uncompressed_size, 0
         else:
@@ -162,7 +176,7 @@ def decompress(source, uncompressed_size=-1, return_bytearray=False, dict=None):
                 raise ValueError(f"Invalid size: 0x{cap}")
             skip = _HDR
         out = bytearray(max(cap, 1))
-        optr = C.addressof((C.c_char * len(out)).from_buffer(out))
+        optr = C.addressof(C.c_char.from_buffer(out))
         sp = _addr(src)
         r = N.lib().lz4m_decompress_safe(None if sp is None else sp + skip, optr, src.nbytes - skip, cap)
         if r < 0:

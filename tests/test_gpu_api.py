@@ -598,3 +598,84 @@ def test_decompress_host_pipelined(gpu):
         if want >= 0:
             o = int(ooff[i])
             assert out[o:o + want].numpy().tobytes() == data[:want], i
+
+
+@pytest.mark.parametrize("kind", ["random", "text", "runs", "zeros"])
+def test_single_call_compress_vs_oracle(gpu, oracle, kind):
+    """lz4m_compress_default / lz4m_compress_block_api (the single-call entry
+    points, include/lz4m.h) against the oracle at sizes on both sides of the
+    LDS-staged lone-block kernel's limit (lz4m_compress_solo: < 65547 bytes,
+    LZ4_64Klimit, lz4.c:689), with full and limited output capacity and
+    accelerations 1 and 7."""
+    import ctypes as C
+    import lz4._native as N
+    from oracle import TABLE_U32_HASH5, compress_bound
+    lib = N.lib()
+    rng = np.random.default_rng(1234)
+    words = [b"lz4", b"block", b"device", b"the", b"wave", b"gfx950", b"stream"]
+
+    def make(n):
+        if kind == "random":
+            return rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        if kind == "zeros":
+            return bytes(n)
+        if kind == "runs":
+            return np.repeat(rng.integers(0, 256, n // 8 + 1, dtype=np.uint8), 8)[:n].tobytes()
+        out = bytearray()
+        while len(out) < n:
+            out += words[int(rng.integers(0, len(words)))] + b" "
+        return bytes(out[:n])
+
+    for n in (0, 1, 13, 100, 4096, 65535, 65536, 65546, 65547, 70000):
+        data = make(n)
+        for accel in (1, 7):
+            for cap in (compress_bound(n), max(n - 1, 0)):
+                dst = C.create_string_buffer(max(cap, 1) + 64)
+                got = lib.lz4m_compress_block_api(data, dst, n, cap, accel)
+                want = oracle.compress(data, variant=TABLE_U32_HASH5, accel=accel, cap=cap)
+                assert (dst.raw[:got] if got > 0 else None) == want, (kind, n, accel, cap, "block_api")
+                if accel == 1:
+                    got = lib.lz4m_compress_default(data, dst, n, cap)
+                    want = oracle.compress(data, variant=None, cap=cap)
+                    assert (dst.raw[:got] if got > 0 else None) == want, (kind, n, cap, "default")
+
+
+def test_single_call_decompress_golden_and_mutated(gpu, golden, oracle):
+    """lz4m_decompress_safe (single call; inputs <= 66 KiB - 64 run the
+    LDS-staged lone-block decoder, lz4m_decompress_solo) returns the
+    reference's status for every golden decompress case (statuses from the
+    compiled reference, tests/golden), and the oracle's status and bytes on
+    mutated and truncated 64 KiB blocks and on an input just past the LDS
+    limit (the batched path)."""
+    import ctypes as C
+    import lz4._native as N
+    lib = N.lib()
+    man, arr = golden
+    for e in man["decompress"]:
+        src = _b(arr, e["key"])
+        out = C.create_string_buffer(max(e["cap"], 1) + 64)
+        assert lib.lz4m_decompress_safe(src, out, len(src), e["cap"]) == e["status"], e
+    rng = np.random.default_rng(77)
+    words = b"".join(rng.choice([b"lz4 ", b"wave ", b"block ", b"hbm ", b"x"], 20000))
+    blocks = [words[:65536], rng.integers(0, 256, 65536, dtype=np.uint8).tobytes(), bytes(65536),
+              np.repeat(rng.integers(0, 256, 8192, dtype=np.uint8), 8).tobytes()]
+    cases = []
+    for blk in blocks:
+        c = oracle.compress(blk)
+        cases.append((c, 65536))
+        for _ in range(40):
+            m = bytearray(c)
+            for _ in range(int(rng.integers(1, 4))):
+                m[int(rng.integers(0, len(m)))] = int(rng.integers(0, 256))
+            cases.append((bytes(m), 65536))
+        cases.append((c[: int(rng.integers(1, len(c)))], 65536))
+        cases.append((c, int(rng.integers(0, 65536))))
+    big = rng.integers(0, 256, 66 * 1024, dtype=np.uint8).tobytes()   # input past the LDS limit
+    cases.append((oracle.compress(big), len(big)))
+    for src, cap in cases:
+        out = C.create_string_buffer(max(cap, 1) + 64)
+        got = lib.lz4m_decompress_safe(src, out, len(src), cap)
+        st, want = oracle.decompress(src, cap)
+        assert got == st, (len(src), cap)
+        if st > 0:
+            assert out.raw[:st] == want[:st]
