@@ -329,6 +329,18 @@ int lz4m_frame_emit(const uint8_t* d_raw, const int64_t* d_raw_off, const int32_
 int lz4m_decompress_safe(const char* src, char* dst, int compressedSize, int dstCapacity);
 int lz4m_compress_default(const char* src, char* dst, int srcSize, int dstCapacity);
 int lz4m_compress_block_api(const char* src, char* dst, int srcSize, int dstCapacity, int acceleration);
+/*
+ * The same two calls with the output left in the calling thread's pinned
+ * staging buffer: *out points at it (valid until the thread's next call), so a
+ * binding builds its result object with one copy (python-lz4's _block.c
+ * allocates the bytes object and copies into it, :230-262, :365-386).
+ * lz4m_compress_block_api_staged with header = 4 also writes the LE32 source
+ * size just before the output (store_size, _block.c:239-243) and *out points
+ * at that header; the return value excludes it.
+ */
+int lz4m_decompress_safe_staged(const char* src, int compressedSize, int dstCapacity, const char** out);
+int lz4m_compress_block_api_staged(const char* src, int srcSize, int dstCapacity, int acceleration, int header,
+                                   const char** out);
 uint32_t lz4m_xxh32(const void* input, size_t length, uint32_t seed);
 
 /*

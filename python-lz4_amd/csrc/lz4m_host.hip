@@ -63,6 +63,7 @@ struct Scratch {
 };
 
 thread_local Scratch t_scratch;
+thread_local const uint8_t* t_out = nullptr;   // the last call's output in the pinned buffer (the _staged calls)
 
 inline size_t up(size_t x) { return (x + 255) & ~(size_t)255; }
 
@@ -99,7 +100,8 @@ int32_t one_block(const char* src, int32_t len, char* dst, int32_t cap, int32_t 
     if (hipMemcpyAsync(h + in, d + in, kMeta + (size_t)cap, hipMemcpyDeviceToHost, s) != hipSuccess) return fail;
     if (hipStreamSynchronize(s) != hipSuccess) return fail;
     memcpy(&m, h + in, sizeof m);
-    if (m.result > 0 && m.result <= cap) memcpy(dst, h + in + kMeta, (size_t)m.result);
+    t_out = h + in + kMeta;
+    if (dst && m.result > 0 && m.result <= cap) memcpy(dst, h + in + kMeta, (size_t)m.result);
     return m.result;
 }
 
@@ -139,14 +141,15 @@ int32_t one_block_mapped(const char* src, int32_t len, char* dst, int32_t cap, i
         __builtin_ia32_pause();
     }
     memcpy(&m, h + in, sizeof m);
-    if (m.result > 0 && m.result <= cap) memcpy(dst, h + in + kMeta, (size_t)m.result);
+    t_out = h + in + kMeta;
+    if (dst && m.result > 0 && m.result <= cap) memcpy(dst, h + in + kMeta, (size_t)m.result);
     return m.result;
 }
 
 // one-block compress through the batched compressors; returns the compressed size or 0
+// dst == nullptr: the output stays in the pinned buffer (t_out), for the _staged calls
 int compress_one(const char* src, char* dst, int srcSize, int dstCapacity, int table, int acceleration) {
-    if (srcSize < 0 || srcSize > kMaxInput || dstCapacity < 0 || (srcSize > 0 && !src) || (dstCapacity > 0 && !dst))
-        return 0;
+    if (srcSize < 0 || srcSize > kMaxInput || dstCapacity < 0 || (srcSize > 0 && !src)) return 0;
     // blocks below 65547 bytes: the LDS-staged lone-block kernel (the
     // skip-ahead search then waits on no memory round trip), no copies
     if (srcSize < kSoloLimit) {
@@ -164,11 +167,8 @@ int compress_one(const char* src, char* dst, int srcSize, int dstCapacity, int t
     return r > 0 ? r : 0;
 }
 
-}  // namespace
-
-extern "C" int lz4m_decompress_safe(const char* src, char* dst, int compressedSize, int dstCapacity) {
-    if (compressedSize < 0 || dstCapacity < 0) return -1;
-    if ((compressedSize > 0 && !src) || (dstCapacity > 0 && !dst)) return -1;
+// dst == nullptr: the output stays in the pinned buffer (t_out), for the _staged calls
+int decompress_one(const char* src, char* dst, int compressedSize, int dstCapacity) {
     // inputs up to 66 KiB - 64 (any 64 KiB block): the LDS-staged lone-block
     // decoder, no copies
     if (compressedSize <= kSoloDecIn)
@@ -184,12 +184,41 @@ extern "C" int lz4m_decompress_safe(const char* src, char* dst, int compressedSi
     });
 }
 
+}  // namespace
+
+extern "C" int lz4m_decompress_safe(const char* src, char* dst, int compressedSize, int dstCapacity) {
+    if (compressedSize < 0 || dstCapacity < 0) return -1;
+    if ((compressedSize > 0 && !src) || (dstCapacity > 0 && !dst)) return -1;
+    return decompress_one(src, dst, compressedSize, dstCapacity);
+}
+
+extern "C" int lz4m_decompress_safe_staged(const char* src, int compressedSize, int dstCapacity, const char** out) {
+    if (compressedSize < 0 || dstCapacity < 0 || !out || (compressedSize > 0 && !src)) return -1;
+    const int r = decompress_one(src, nullptr, compressedSize, dstCapacity);
+    *out = reinterpret_cast<const char*>(t_out);
+    return r;
+}
+
 extern "C" int lz4m_compress_default(const char* src, char* dst, int srcSize, int dstCapacity) {
+    if (dstCapacity > 0 && !dst) return 0;
     return compress_one(src, dst, srcSize, dstCapacity, LZ4M_TABLE_AUTO, 1);
 }
 
 extern "C" int lz4m_compress_block_api(const char* src, char* dst, int srcSize, int dstCapacity, int acceleration) {
+    if (dstCapacity > 0 && !dst) return 0;
     return compress_one(src, dst, srcSize, dstCapacity, LZ4M_TABLE_U32_HASH5, acceleration);
+}
+
+extern "C" int lz4m_compress_block_api_staged(const char* src, int srcSize, int dstCapacity, int acceleration,
+                                              int header, const char** out) {
+    if (!out || (header != 0 && header != 4)) return 0;
+    const int r = compress_one(src, nullptr, srcSize, dstCapacity, LZ4M_TABLE_U32_HASH5, acceleration);
+    if (r > 0 && header) {   // the LE32 size just before the output, in the call record's slack (kMeta)
+        uint8_t* p = const_cast<uint8_t*>(t_out) - 4;
+        for (int k = 0; k < 4; ++k) p[k] = (uint8_t)((uint32_t)srcSize >> (8 * k));
+    }
+    *out = reinterpret_cast<const char*>(t_out) - header;
+    return r;
 }
 
 extern "C" uint32_t lz4m_xxh32(const void* input, size_t length, uint32_t seed) {

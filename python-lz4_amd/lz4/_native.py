@@ -68,6 +68,8 @@ def _declare(lib) -> None:
         "lz4m_decompress_safe": ([vp, vp, i32, i32], i32),
         "lz4m_compress_default": ([vp, vp, i32, i32], i32),
         "lz4m_compress_block_api": ([vp, vp, i32, i32, i32], i32),
+        "lz4m_decompress_safe_staged": ([vp, i32, i32, C.POINTER(vp)], i32),
+        "lz4m_compress_block_api_staged": ([vp, i32, i32, i32, i32, C.POINTER(vp)], i32),
         "lz4m_xxh32": ([vp, C.c_size_t, u32], u32),
         "lz4m_xxh32_host_reset": ([vp, u32], None),
         "lz4m_xxh32_host_update": ([vp, vp, C.c_size_t], None),

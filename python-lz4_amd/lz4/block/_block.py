@@ -127,15 +127,14 @@ def compress(source, mode="default", store_size=True, acceleration=1, compressio
         N.require_device()
         n = src.nbytes
         hdr = _HDR if store_size else 0
-        out = bytearray(hdr + max(N.compress_bound(n), 1))
-        optr = C.addressof(C.c_char.from_buffer(out))
-        r = N.lib().lz4m_compress_block_api(_addr(src), optr + hdr, n, len(out) - hdr, accel)
+        p = C.c_void_p()
+        # the output (after the size header) stays in the thread's pinned buffer: one copy into the result
+        r = N.lib().lz4m_compress_block_api_staged(_addr(src), n, max(N.compress_bound(n), 1), accel, hdr,
+                                                   C.byref(p))
         if r <= 0:
             raise LZ4BlockError("Compression failed")
-        if hdr:
-            out[:4] = n.to_bytes(4, "little")
-        del out[hdr + r:]
-        return out if return_bytearray else bytes(out)
+        out = C.string_at(p.value, hdr + r)
+        return bytearray(out) if return_bytearray else out
     # dictionary memory that ends where the source begins: the reference's
     # LZ4_compress_fast_continue sees dictEnd == source and takes prefix mode
     # (lz4.c:1671-1676; LZ4_loadDict keeps no dictionary below 8 bytes)
@@ -175,18 +174,18 @@ def decompress(source, uncompressed_size=-1, return_bytearray=False, dict=None):
             if cap > INT_MAX:
                 raise ValueError(f"Invalid size: 0x{cap}")
             skip = _HDR
-        out = bytearray(max(cap, 1))
-        optr = C.addressof(C.c_char.from_buffer(out))
         sp = _addr(src)
-        r = N.lib().lz4m_decompress_safe(None if sp is None else sp + skip, optr, src.nbytes - skip, cap)
+        p = C.c_void_p()
+        # the output stays in the thread's pinned buffer: one copy into the result
+        r = N.lib().lz4m_decompress_safe_staged(None if sp is None else sp + skip, src.nbytes - skip, cap, C.byref(p))
         if r < 0:
             raise LZ4BlockError(
                 "Decompression failed: corrupt input or insufficient space in destination buffer. "
                 f"Error code: {-r}")
         if r != cap and uncompressed_size < 0:
             raise LZ4BlockError(f"Decompressor wrote {r} bytes, but {cap} bytes expected from header")
-        del out[r:]
-        return out if return_bytearray else bytes(out)
+        out = C.string_at(p.value, r) if r else b""
+        return bytearray(out) if return_bytearray else out
     res = decompress_many([src], uncompressed_size=uncompressed_size, dict=dview,
                           as_bytearray=bool(return_bytearray), raise_errors=True)
     return res[0]
