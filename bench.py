@@ -82,33 +82,66 @@ def compress_all(src: torch.Tensor, n: int, table: int, dev, events=None):
     return (src_off, src_len, dst, dst_off, dst_cap, out_len)
 
 
-def time_kernel(fn, steps: int, warmup: int, world: int):
+class _HostEvent:
+    """torch.cuda.Event's timing interface on the host clock (CPU runs of the
+    timing helpers: tests/test_bench_dist.py)."""
+
+    def __init__(self):
+        self.t = 0.0
+
+    def record(self):
+        self.t = time.perf_counter()
+
+    def elapsed_time(self, end) -> float:
+        return (end.t - self.t) * 1e3
+
+
+def time_kernel(fn, steps: int, warmup: int, world: int, device: str = "cuda"):
     """Warmup, then time exactly `steps` calls bracketed by barrier+sync;
-    returns (wall seconds max over ranks, mean per-launch seconds from HIP
-    events recorded on the launch stream)."""
+    returns (wall seconds, mean per-launch seconds from HIP events recorded on
+    the launch stream), each the MAX over ranks.  device="cpu" runs the same
+    protocol on the host clock (gloo process groups, CPU tests)."""
+    cuda = device == "cuda"
+
+    def sync():
+        if cuda:
+            torch.cuda.synchronize()
+
     for _ in range(warmup):
         fn()
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         torch.distributed.barrier()
-    torch.cuda.synchronize()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    sync()
+    ev = (lambda: torch.cuda.Event(enable_timing=True)) if cuda else _HostEvent
+    evs = [(ev(), ev()) for _ in range(steps)]
     t0 = time.perf_counter()
     for a, b in evs:
         a.record()
         fn()
         b.record()
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         torch.distributed.barrier()
-    torch.cuda.synchronize()
+    sync()
     wall = time.perf_counter() - t0
     ev_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
     if world > 1:
-        t = torch.tensor([wall, ev_ms], dtype=torch.float64, device="cuda")
+        t = torch.tensor([wall, ev_ms], dtype=torch.float64, device=device)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         wall, ev_ms = float(t[0]), float(t[1])
     return wall, ev_ms / 1e3
+
+
+def aggregate_gib_s(world: int, units_per_rank: int, unit_bytes: int, wall_s: float, steps: int) -> float:
+    """Whole-job rate: the bytes ALL ranks processed (weak scaling: every
+    rank the same units) over the max-over-ranks time of one step."""
+    return world * units_per_rank * unit_bytes / (wall_s / steps) / GIB
+
+
+def runs_cpu_baseline(rank: int, no_cpu: bool) -> bool:
+    """The CPU baseline is timed on rank 0 only (its host cores), once."""
+    return rank == 0 and not no_cpu
 
 
 def host_threads() -> int:
@@ -430,7 +463,7 @@ def main():
     c_off = offs[:n].clone()
     c_len = out_len.clone()
     comp_sample = None
-    if rank == 0 and not args.no_cpu:   # cpu_baseline at every N (rank 0, after the timed regions)
+    if runs_cpu_baseline(rank, args.no_cpu):   # cpu_baseline at every N (rank 0, after the timed regions)
         k = min(n, 16384)
         comp_host_np = comp[: int(offs[k])].cpu().numpy()
         oh = offs[: k + 1].cpu().numpy()
@@ -614,7 +647,7 @@ def main():
 
     # ---- report ----
     d_step = d_wall / args.steps
-    value = world * n * BLOCK / d_step / GIB
+    value = aggregate_gib_s(world, n, BLOCK, d_wall, args.steps)
     algo_bytes = comp_total + n * BLOCK          # per launch: read compressed + write decoded
     achieved = algo_bytes / d_ev / 1e9           # GB/s, from HIP events on the launch stream
     # HBM bytes per launch of the decoder from the committed PMC summary of

@@ -199,6 +199,35 @@ __device__ __forceinline__ void lds_put_al(lds_u8* p, u32x4 v, int32_t k, lds_cu
 #endif
 }
 
+// ------------------------------------------------ period-pattern selectors
+// A match with offset off < 16 repeats its first off bytes: output byte j is
+// w[j % off] (LZ4_memcpy_using_offset, lz4.c:513-551).  Selector table: 8
+// dwords per offset (16 x 8 = 128), entry (off, i) builds output dword i >> 1
+// from bytes 0-7 (i even) or 8-15 (i odd) of w; 0x0C selects a zero byte.
+__device__ __forceinline__ void period_sel_init(uint32_t* psel, uint32_t tid, uint32_t nthreads) {
+    for (uint32_t e = tid; e < 16u * 8u; e += nthreads) {
+        const uint32_t o = e >> 3, i = e & 7, hi = i & 1;
+        uint32_t v = 0;
+        for (uint32_t b = 0; b < 4; ++b) {
+            const uint32_t x = o ? (4 * (i >> 1) + b) % o : 0;
+            const uint32_t sb = hi ? (x >= 8 ? x - 8 : 0x0C) : (x < 8 ? x : 0x0C);
+            v |= sb << (8 * b);
+        }
+        psel[e] = v;
+    }
+}
+// Period-off pattern of the first off (1..15) bytes of w, E[j] = w[j % off]:
+// per output dword, v_perm from bytes 0-7 and from bytes 8-15 with the
+// selectors sel = psel + 8 * off.
+__device__ __forceinline__ u32x4 period_perm(u32x4 w, lds_cu32* sel) {
+    u32x4 r;
+    r.x = __builtin_amdgcn_perm(w.y, w.x, sel[0]) | __builtin_amdgcn_perm(w.w, w.z, sel[1]);
+    r.y = __builtin_amdgcn_perm(w.y, w.x, sel[2]) | __builtin_amdgcn_perm(w.w, w.z, sel[3]);
+    r.z = __builtin_amdgcn_perm(w.y, w.x, sel[4]) | __builtin_amdgcn_perm(w.w, w.z, sel[5]);
+    r.w = __builtin_amdgcn_perm(w.y, w.x, sel[6]) | __builtin_amdgcn_perm(w.w, w.z, sel[7]);
+    return r;
+}
+
 __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 
 __device__ __forceinline__ int64_t readlane64(int64_t v, int lane) {

@@ -751,6 +751,10 @@ __global__ __launch_bounds__(256) void compress_solo_kernel(const uint8_t* __res
         }
     }
     if (h_done != nullptr) {   // all of the above visible to the host, then the flag it polls
+        // every storing thread releases its own h_out stores at system scope
+        // (a workgroup barrier alone does not wait for other waves' stores to
+        // reach memory: ADVICE r03); then one thread stores the flag
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
         __syncthreads();
         if (t == 0) __hip_atomic_store(h_done, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }

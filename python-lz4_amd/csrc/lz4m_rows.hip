@@ -677,18 +677,6 @@ __device__ __forceinline__ void load32(const uint8_t* s, int32_t t, int32_t iend
 }
 
 
-// Period-`off` pattern of the first off (1..15) bytes of w, E[j] = w[j % off]:
-// per output dword, v_perm from bytes 0-7 and from bytes 8-15 with
-// selectors from the table `sel` (8 dwords per offset; 0x0C selects zero).
-__device__ __forceinline__ u32x4 period_perm(u32x4 w, lds_cu32* sel) {
-    u32x4 r;
-    r.x = __builtin_amdgcn_perm(w.y, w.x, sel[0]) | __builtin_amdgcn_perm(w.w, w.z, sel[1]);
-    r.y = __builtin_amdgcn_perm(w.y, w.x, sel[2]) | __builtin_amdgcn_perm(w.w, w.z, sel[3]);
-    r.z = __builtin_amdgcn_perm(w.y, w.x, sel[4]) | __builtin_amdgcn_perm(w.w, w.z, sel[5]);
-    r.w = __builtin_amdgcn_perm(w.y, w.x, sel[6]) | __builtin_amdgcn_perm(w.w, w.z, sel[7]);
-    return r;
-}
-
 // One round of a row, parsed: lane jj's sequence (literal at input position
 // t, lit / off / ml), its output position o, the round's row totals and the
 // far source requested from HBM; the literal's first 32 bytes go to XS.
@@ -842,17 +830,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LZ4M_ROWS_WA
 #else
     lds_u8* DUM = (lds_u8*)(dums + lane * 16);
 #endif
-    // period selectors: entry (off, i) for output dword i>>1, bytes 0-7 (i even) or 8-15
-    for (int e = (int)lane; e < 16 * 8; e += 64) {
-        const uint32_t o = (uint32_t)e >> 3, i = (uint32_t)e & 7, hi = i & 1;
-        uint32_t v = 0;
-        for (uint32_t b = 0; b < 4; ++b) {
-            const uint32_t x = o ? (4 * (i >> 1) + b) % o : 0;
-            const uint32_t sb = hi ? (x >= 8 ? x - 8 : 0x0C) : (x < 8 ? x : 0x0C);
-            v |= sb << (8 * b);
-        }
-        psel[e] = v;
-    }
+    period_sel_init(psel, lane, 64);
     lds_cu32* PS = (lds_cu32*)psel;
     lds_u32x4* XSL = (lds_u32x4*)(xsl + 2 * lane);
     // this lane's dummy store target (flush stores of lanes with nothing final)
@@ -1177,6 +1155,24 @@ extern "C" int lz4m_rows_launch(const uint8_t* d_src, const int64_t* d_src_off, 
                        d_src_len, d_dst_cap, n, meta, lens, lens_cap, ctr);
     hipLaunchKernelGGL(rows_exec_kernel, dim3((uint32_t)exec_grid), dim3(64), 0, stream, d_src, d_src_off, d_src_len,
                        d_dst, d_dst_off, meta, lens, n, ctr);
+    return (int)hipGetLastError();
+}
+
+// the parse alone (counters zeroed first): the block-resident executor
+// (lz4m_resident.hip) reads the same records and length bytes
+extern "C" int lz4m_rows_parse_launch(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len,
+                                      const int32_t* d_dst_cap, int64_t n, void* d_work, size_t work_bytes,
+                                      int parse_grid, hipStream_t stream) {
+    const size_t fixed = lz4m_rows_fixed_bytes(n);
+    if (work_bytes < fixed) return LZ4M_ROWS_ENOSPACE;
+    unsigned long long* ctr = static_cast<unsigned long long*>(d_work);
+    RowMeta* meta = reinterpret_cast<RowMeta*>(static_cast<uint8_t*>(d_work) + kRowsMeta);
+    uint8_t* lens = static_cast<uint8_t*>(d_work) + fixed;
+    const int64_t lens_cap = (int64_t)(work_bytes - fixed);
+    hipError_t e = hipMemsetAsync(ctr, 0, 64, stream);
+    if (e != hipSuccess) return (int)e;
+    hipLaunchKernelGGL(rows_parse_kernel, dim3((uint32_t)parse_grid), dim3(kPWG), 0, stream, d_src, d_src_off,
+                       d_src_len, d_dst_cap, n, meta, lens, lens_cap, ctr);
     return (int)hipGetLastError();
 }
 
