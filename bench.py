@@ -626,6 +626,26 @@ def main():
             "decompress_frame_no_content_checksum_gib_s": round(world * L / fn_wall / GIB, 2),
             "note": "content XXH32 is one serial stream (SURVEY 0.5): a host core hashes the bytes streamed back "
                     "over PCIe while the device compresses / decodes (lz4m_xxh32_host_*)"}
+        # the drop-in call itself: lz4.frame.compress / decompress on the caller's
+        # host bytes -- the exact parse (blocks byte-identical to LZ4F_compressFrame's), 4 MiB
+        # independent blocks, content checksum (_frame.c:226-228 -> lz4frame.c:475-515; decode
+        # lz4frame.c:1556-2058) -- host bytes in, host bytes out, PCIe included
+        if world == 1:
+            hb = fsrc.cpu().numpy().tobytes()
+            kw4 = dict(block_size=F.BLOCKSIZE_MAX4MB, block_linked=False, content_checksum=True)
+            F.decompress(F.compress(hb[: 64 << 20], **kw4))   # warm-up: kernels, pinned staging
+            dbox = {}
+            di_wall, _ = time_kernel(lambda: dbox.__setitem__("f", F.compress(hb, **kw4)), 1, 0, world)
+            fr_h = dbox.pop("f")
+            do_wall, _ = time_kernel(lambda: dbox.__setitem__("d", F.decompress(fr_h)), 1, 0, world)
+            assert dbox.pop("d") == hb, "drop-in config-4 frame does not round-trip"
+            assert len(fr_h) == ex_len + 4, "drop-in frame size differs from the exact-parse frame (+ content checksum)"
+            extra["frame4m"]["dropin_compress_gib_s"] = round(L / di_wall / GIB, 2)
+            extra["frame4m"]["dropin_decompress_gib_s"] = round(L / do_wall / GIB, 2)
+            extra["frame4m"]["dropin_note"] = ("lz4.frame.compress(bytes, block_size=BLOCKSIZE_MAX4MB, block_linked=False, "
+                                               "content_checksum=True) and lz4.frame.decompress of its result: host bytes "
+                                               "in and out, exact parse, PCIe and the serial content XXH32 included")
+            del hb, fr_h
         # lz4.frame.compress's defaults (64 KiB linked blocks, the exact parse, byte-identical to the
         # reference): speculative-parallel linked compression on a 256 MiB sample of the same input
         LS = min(L, 256 << 20)

@@ -320,9 +320,15 @@ int lz4m_frame_emit(const uint8_t* d_raw, const int64_t* d_raw_off, const int32_
 /*
  * Single-buffer, HOST-pointer functions with the lz4.h contracts, for a C
  * caller replacing the reference's per-call lz4libs functions one for one
- * (lz4m_host.hip).  Each copies to the device, runs the batched kernel on a
- * batch of one and copies back (synchronous; device scratch cached per
- * thread).  Throughput comes from the batched functions above.
+ * (lz4m_host.hip).  Synchronous.  A block of up to 64 KiB (compress: below
+ * LZ4_64Klimit; decompress: input below 66 KiB) is one launch of a lone-block
+ * kernel (lz4m_compress_solo / lz4m_decompress_solo) that reads the input and
+ * its call record from the thread's mapped pinned staging buffer, stages the
+ * block in LDS, writes the result back into that buffer itself and releases a
+ * done flag the host polls: no stream copies.  Larger inputs copy to the
+ * device, run the batched kernel on a batch of one and copy back (device
+ * scratch cached per thread).  Throughput comes from the batched functions
+ * above.
  *   lz4m_decompress_safe    = LZ4_decompress_safe (lz4.h:191-205)
  *                             replaces _block.c:357-359 with dict size 0;
  *   lz4m_compress_default   = LZ4_compress_default (lz4.h:175-189);
@@ -363,6 +369,14 @@ void lz4m_xxh32_host_reset(lz4m_xxh32_state* state, uint32_t seed);
 void lz4m_xxh32_host_update(lz4m_xxh32_state* state, const void* input, size_t length);
 uint32_t lz4m_xxh32_host_digest(const lz4m_xxh32_state* state);
 uint32_t lz4m_xxh32_host(const void* input, size_t length, uint32_t seed);
+
+/* Host memcpy of n bytes split over `threads` threads (1..16; one below
+ * 4 MiB); when `hash` is not NULL, one more thread runs
+ * lz4m_xxh32_host_update(hash, src, n) over the same source meanwhile.  The
+ * staging copies of the drop-in frame calls (lz4.frame.compress / decompress
+ * on host bytes, _frame.c:226-228, :1058-1063) and their content checksum
+ * (lz4frame.c:1042, :1850) in one pass. */
+void lz4m_host_copy(void* dst, const void* src, size_t n, int threads, lz4m_xxh32_state* hash);
 
 /*
  * Block-record walk of an LZ4 frame already in device memory

@@ -1,11 +1,14 @@
 // lz4m_host.hip -- single-buffer, host-pointer entry points with the lz4.h
 // contracts, for a C caller that replaces the
 // reference's per-call lz4libs functions one for one (e.g. a rebuilt
-// lz4/block/_block.c).  Each call copies its input to the device, runs the
-// batched kernel on a batch of one, and copies the result back; device
-// buffers are cached per thread and grow as needed.  These are convenience
-// wrappers: throughput comes from the batched entry points, a single
-// 64 KiB block is latency-bound on one lane.
+// lz4/block/_block.c).  A block of up to 64 KiB is one launch of a lone-block
+// kernel on mapped pinned memory (one_block_mapped: the kernel reads the
+// caller's bytes and the call record from the thread's pinned staging buffer,
+// stages the block in LDS, writes the result back itself and releases a done
+// flag that the host polls).  Larger inputs copy to
+// the device, run the batched kernel on a batch of one and copy the result
+// back; device buffers are cached per thread and grow as needed.  Throughput
+// comes from the batched entry points.
 #include "../../include/lz4m.h"
 
 #include <hip/hip_runtime.h>

@@ -41,7 +41,10 @@
 
 namespace lz4m {
 
-constexpr int kResW = 4;                      // waves per workgroup (one block)
+#ifndef LZ4M_RES_W
+#define LZ4M_RES_W 4
+#endif
+constexpr int kResW = LZ4M_RES_W;             // waves per workgroup (one block)
 constexpr int kResT = 64 * kResW;             // threads per workgroup
 constexpr int32_t kResOut = 65536;            // output bytes held in LDS
 constexpr int32_t kResLim = kResOut - 64;     // placed sequences end at or below this
@@ -103,13 +106,6 @@ __device__ __forceinline__ uint32_t slot_wait(lds_vu64a* s, uint32_t tag, uint32
 // ---------------------------------------------------- written-byte bitmap
 // bits r .. r + L - 1 (1 <= L <= 32, 0 <= r <= 31) of a 64-bit pair
 __device__ __forceinline__ uint64_t span_mask(int32_t r, int32_t L) { return (((uint64_t)1 << L) - 1) << r; }
-// every byte of [p, p + L) written (1 <= L <= 32)
-__device__ __forceinline__ bool bits_all(lds_vu32a* B, int32_t p, int32_t L) {
-    const int32_t k = p >> 5;
-    const uint64_t w = (uint64_t)B[k] | ((uint64_t)B[k + 1] << 32);
-    const uint64_t msk = span_mask(p & 31, L);
-    return (w & msk) == msk;
-}
 // ds_or_b32 (no return): issued after the bytes' own writes, in this wave's
 // LDS order, so a reader that sees the bit reads the bytes
 #define LZ4M_DSOR(addr, x) asm volatile("ds_or_b32 %0, %1" ::"v"(addr), "v"(x) : "memory")
@@ -137,6 +133,74 @@ __device__ __forceinline__ void bits_fill_wave(lds_vu32a* B, int32_t p, int32_t 
         const uint32_t m = hi - lo >= 32 ? ~0u : ((1u << (hi - lo)) - 1u) << lo;
         LZ4M_DSOR(lds_addr((const lds_u8*)(B + k)), m);
     }
+}
+
+// ------------------------------------------------ one-round-trip LDS access
+// A match attempt needs the written-byte bits of its source and the source
+// bytes, read in that order (a reader that sees a bit must read the byte
+// after it).  Both are issued back to back and waited for once: the bits of
+// [p, p + 32) (two dwords) and the 40 bytes at p & ~7 (five aligned 8-byte
+// reads: any 32-byte window at p).  The compiler knows nothing of these
+// loads, hence the explicit wait inside the asm.
+struct SrcRead {
+    uint64_t bits, w0, w1, w2, w3, w4;
+};
+__device__ __forceinline__ void src_read(uint32_t baddr, uint32_t daddr, SrcRead& r) {
+    // volatile: issued in program order (bits first); the empty asm after the
+    // last one is a scheduling boundary, so nothing that waits for the bits
+    // is placed between the loads
+    typedef __attribute__((address_space(3))) volatile uint32_t vu32;
+    const vu32* B = (const vu32*)(uintptr_t)baddr;
+    const lds_vu64a* D = (const lds_vu64a*)(uintptr_t)daddr;
+    const uint32_t b0 = B[0], b1 = B[1];
+    r.w0 = D[0];
+    r.w1 = D[1];
+    r.w2 = D[2];
+    r.w3 = D[3];
+    r.w4 = D[4];
+    asm volatile("" ::: "memory");
+    r.bits = (uint64_t)b0 | ((uint64_t)b1 << 32);
+}
+// 16 bytes at byte q (0..7) of the 24-byte run x0|x1|x2
+__device__ __forceinline__ u32x4 funnel16(uint64_t x0, uint64_t x1, uint64_t x2, uint32_t q) {
+    const bool h = (q & 4u) != 0;
+    const uint32_t r = q & 3u;
+    const uint32_t c0 = (uint32_t)x0, c1 = (uint32_t)(x0 >> 32), c2 = (uint32_t)x1, c3 = (uint32_t)(x1 >> 32),
+                   c4 = (uint32_t)x2, c5 = (uint32_t)(x2 >> 32);
+    const uint32_t e0 = h ? c1 : c0, e1 = h ? c2 : c1, e2 = h ? c3 : c2, e3 = h ? c4 : c3, e4 = h ? c5 : c4;
+    return u32x4{__builtin_amdgcn_alignbyte(e1, e0, r), __builtin_amdgcn_alignbyte(e2, e1, r),
+                 __builtin_amdgcn_alignbyte(e3, e2, r), __builtin_amdgcn_alignbyte(e4, e3, r)};
+}
+// are the bits r .. r + L - 1 (1 <= L <= 32, 0 <= r <= 31) of w all set
+__device__ __forceinline__ bool bits_in(uint64_t w, int32_t r, int32_t L) {
+    const uint64_t msk = span_mask(r, L);
+    return (w & msk) == msk;
+}
+// mask of the low n (0..4) bytes of a dword
+__device__ __forceinline__ uint32_t low_bytes(int32_t n) { return n >= 4 ? ~0u : ((1u << (8 * n)) - 1u); }
+// Exactly k (>= 1; >= 16: 16) bytes of v at LDS byte address a: five masked
+// ORs on the enclosing aligned dwords (atomic per dword, so neighbouring
+// sequences sharing a dword may write it at once), masks computed in
+// registers (no table read: one LDS round trip less per put).
+__device__ __forceinline__ void lds_put_ar(uint32_t a, u32x4 v, int32_t k) {
+    const uint32_t r = a & 3u;
+    const int32_t e = (int32_t)r + min(k, 16);
+    const uint32_t s = (4u - r) & 3u;
+    const bool z = r == 0;
+    const uint32_t d0 = __builtin_amdgcn_alignbyte(v.x, z ? v.x : 0u, s);
+    const uint32_t d1 = __builtin_amdgcn_alignbyte(v.y, z ? v.y : v.x, s);
+    const uint32_t d2 = __builtin_amdgcn_alignbyte(v.z, z ? v.z : v.y, s);
+    const uint32_t d3 = __builtin_amdgcn_alignbyte(v.w, z ? v.w : v.z, s);
+    const uint32_t d4 = __builtin_amdgcn_alignbyte(0u, z ? 0u : v.w, s);
+    const uint32_t m0 = low_bytes(min(e, 4)) & ~low_bytes((int32_t)r);
+    const uint32_t m1 = low_bytes(min(max(e - 4, 0), 4)), m2 = low_bytes(min(max(e - 8, 0), 4));
+    const uint32_t m3 = low_bytes(min(max(e - 12, 0), 4)), m4 = low_bytes(max(e - 16, 0));
+    const uint32_t b4 = a & ~3u;
+    LZ4M_MSKOR(b4, 0, m0, d0);
+    LZ4M_MSKOR(b4, 4, m1, d1);
+    LZ4M_MSKOR(b4, 8, m2, d2);
+    LZ4M_MSKOR(b4, 12, m3, d3);
+    LZ4M_MSKOR(b4, 16, m4, d4);
 }
 
 // ------------------------------------------------------------- sequences
@@ -265,7 +329,7 @@ __device__ __forceinline__ void res_gput(uint8_t* p, u32x4 v, int32_t k) {
 }
 
 // ------------------------------------------------------------ the kernel
-__global__ __launch_bounds__(kResT, 2) void res_exec_kernel(const uint8_t* __restrict__ src,
+__global__ __launch_bounds__(kResT, kResW / 2) void res_exec_kernel(const uint8_t* __restrict__ src,
                                                            const int64_t* __restrict__ src_off,
                                                            const int32_t* __restrict__ src_len, uint8_t* dst,
                                                            const int64_t* __restrict__ dst_off, RowMeta* meta,
@@ -273,22 +337,17 @@ __global__ __launch_bounds__(kResT, 2) void res_exec_kernel(const uint8_t* __res
                                                            unsigned long long* __restrict__ ctr) {
     __shared__ __attribute__((aligned(16))) uint8_t outb[kResOut + 64];
     __shared__ __attribute__((aligned(16))) uint32_t bitw[kResBitW];
-    __shared__ __attribute__((aligned(16))) uint32_t mtab[kPutTab];
-    __shared__ __attribute__((aligned(16))) uint32_t psel[16 * 8];
     __shared__ __attribute__((aligned(16))) uint64_t slots[8];   // 0-3: input positions, 4-7: output positions
     __shared__ int64_t nxt_s;                                     // the next block
     __shared__ int32_t opg_s;                                     // the block's good output end (after a cut)
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
-    lds_put_table_init(mtab, tid, kResT);
-    period_sel_init(psel, tid, kResT);
     for (int k = (int)tid; k < kResBitW; k += kResT) bitw[k] = 0;
     if (tid < 8) slots[tid] = 0;
     if (tid == 0) nxt_s = (int64_t)atomicAdd(&ctr[2], 1ull);
     __syncthreads();
     lds_u8* OUT = (lds_u8*)outb;
     lds_vu32a* B = (lds_vu32a*)bitw;
-    lds_cu32* MT = (lds_cu32*)mtab;
-    lds_cu32* PS = (lds_cu32*)psel;
+    const uint32_t obase = lds_addr(OUT), bbase = lds_addr((const lds_u8*)B);
     lds_vu64a* IPS = (lds_vu64a*)slots;
     lds_vu64a* OPS = IPS + 4;
     RS_DECL
@@ -350,19 +409,18 @@ __global__ __launch_bounds__(kResT, 2) void res_exec_kernel(const uint8_t* __res
             PSet S0, S1, S2;
             int32_t L0 = 0, L1 = 0, L2;
             {
-                const int32_t l0 = lens_at((int32_t)wv), l1 = lens_at((int32_t)wv + 4);
+                const int32_t l0 = lens_at((int32_t)wv), l1 = lens_at((int32_t)wv + kResW);
                 prepare((int32_t)wv, l0, S0.t, S0.clen, S0.a, S0.b);
-                prepare((int32_t)wv + 4, l1, S1.t, S1.clen, S1.a, S1.b);
+                prepare((int32_t)wv + kResW, l1, S1.t, S1.clen, S1.a, S1.b);
             }
-            L2 = lens_at((int32_t)wv + 8);
-            // one chunk: execute set P (chunk c), prepare chunk c + 8 into set Q
-            // with the length byte Lu, request chunk c + 12's into Ll
+            L2 = lens_at((int32_t)wv + 2 * kResW);
+            // one chunk: execute set P (chunk c), prepare chunk c + 2W into set Q
+            // with the length byte Lu, request chunk c + 3W's into Ll
             auto iter = [&](int32_t c, PSet& P, PSet& Q, int32_t& Lu, int32_t& Ll) __attribute__((always_inline)) {
                 RS_MARK(0);
                 RS_COUNT(10, 1);
                 const int32_t t0 = P.t, c0 = P.clen;
                 const u32x4 a0 = P.a, b0 = P.b;
-                Ll = lens_at(c + 12);
                 const int32_t cnt = min(64, nseq - 64 * c);
                 bool act = (int32_t)lane < cnt;
                 ResSeq q;
@@ -401,16 +459,16 @@ __global__ __launch_bounds__(kResT, 2) void res_exec_kernel(const uint8_t* __res
                         const uint32_t sh = (uint32_t)q.lp;
                         const u32x4 x0{__builtin_amdgcn_alignbyte(a0.y, a0.x, sh), __builtin_amdgcn_alignbyte(a0.z, a0.y, sh),
                                        __builtin_amdgcn_alignbyte(a0.w, a0.z, sh), __builtin_amdgcn_alignbyte(b0.x, a0.w, sh)};
-                        lds_put_al(OUT + o, x0, q.lit, MT);
+                        lds_put_ar(obase + (uint32_t)o, x0, q.lit);
                         if (q.lit > 16) {
                             const u32x4 x1{__builtin_amdgcn_alignbyte(b0.y, b0.x, sh), __builtin_amdgcn_alignbyte(b0.z, b0.y, sh),
                                            __builtin_amdgcn_alignbyte(b0.w, b0.z, sh), __builtin_amdgcn_alignbyte(0u, b0.w, sh)};
-                            lds_put_al(OUT + o + 16, x1, q.lit - 16, MT);
+                            lds_put_ar(obase + (uint32_t)o + 16u, x1, q.lit - 16);
                         }
                     } else {
                         // good long literals end >= 32 bytes before the block end (lz4.c:2016-2027)
                         for (int32_t i = 0; i < q.lit; i += 16)
-                            lds_put_al(OUT + o + i, ld16(s + min(t0 + q.lp + i, iend - 16)), q.lit - i, MT);
+                            lds_put_ar(obase + (uint32_t)(o + i), ld16(s + min(t0 + q.lp + i, iend - 16)), q.lit - i);
                     }
                     bits_fill(B, o, q.lit);
                 }
@@ -420,13 +478,10 @@ __global__ __launch_bounds__(kResT, 2) void res_exec_kernel(const uint8_t* __res
                     const uint8_t* se = s + __builtin_amdgcn_readlane(t0 + q.lp, e);
                     const int32_t lim = iend - 16 - __builtin_amdgcn_readlane(t0 + q.lp, e);
                     for (int32_t x = 16 * (int32_t)lane; x < le; x += 16 * 64)
-                        lds_put_al(OUT + oe + x, ld16(se + min(x, lim)), le - x, MT);
+                        lds_put_ar(obase + (uint32_t)(oe + x), ld16(se + min(x, lim)), le - x);
                     bits_fill_wave(B, oe, le, lane);
                 }
                 RS_MARK(3);
-                // ---- the chunk two ahead: its input positions and bytes
-                prepare(c + 2 * kResW, Lu, Q.t, Q.clen, Q.a, Q.b);
-                RS_MARK(4);
                 // ---- matches: each copies once every source byte is written
                 const int32_t m = o + q.lit, off = q.off, ml = q.ml, s0 = m - off;
                 const bool per = off < 16;   // period pattern
@@ -438,20 +493,23 @@ __global__ __launch_bounds__(kResT, 2) void res_exec_kernel(const uint8_t* __res
                     if (pend && !lng) {
                         const int32_t sp = per ? s0 : s0 + dn;
                         const int32_t L = per ? off : min(min(32, ml - dn), off);
-                        const bool ready = bits_all(B, sp, L);
-                        const u32x4 v0 = lds_ld16a(OUT + sp);   // read after the bits: final if they are set
-                        if (ready) {
-                            if (per) {
-                                const u32x4 pat = period_perm(v0, PS + 8 * off);
+                        // the source's bits, then its bytes: one round trip
+                        SrcRead rd;
+                        src_read(bbase + 4u * (uint32_t)(sp >> 5), obase + ((uint32_t)sp & ~7u), rd);
+                        if (bits_in(rd.bits, sp & 31, L)) {
+                            const uint32_t q8 = (uint32_t)sp & 7u;
+                            const u32x4 v0 = funnel16(rd.w0, rd.w1, rd.w2, q8);
+                            if (per) {   // period pattern of the first off bytes
+                                const u32x4 pat = period_pattern(v0, (uint32_t)off);
                                 const int32_t stp = 16 - 16 % off;
                                 const int32_t w = ml <= kResLong ? ml : 64;   // the rest on the whole wave
-                                for (int32_t i = 0; i < w; i += stp) lds_put_al(OUT + m + i, pat, w - i, MT);
+                                for (int32_t i = 0; i < w; i += stp) lds_put_ar(obase + (uint32_t)(m + i), pat, w - i);
                                 bits_fill(B, m, w);
                                 dn = w;
-                                lng = true;   // any rest: on the whole wave (this lane's attempt restarts at s0)
+                                lng = true;   // any rest: on the whole wave
                             } else {
-                                lds_put_al(OUT + m + dn, v0, L, MT);
-                                if (L > 16) lds_put_al(OUT + m + dn + 16, lds_ld16a(OUT + sp + 16), L - 16, MT);
+                                lds_put_ar(obase + (uint32_t)(m + dn), v0, L);
+                                if (L > 16) lds_put_ar(obase + (uint32_t)(m + dn + 16), funnel16(rd.w2, rd.w3, rd.w4, q8), L - 16);
                                 bits_set(B, m + dn, L);
                                 dn += L;
                             }
@@ -473,10 +531,12 @@ __global__ __launch_bounds__(kResT, 2) void res_exec_kernel(const uint8_t* __res
                         const int32_t x = 16 * (int32_t)lane;
                         const bool pc = x < W && x < rem;
                         const int32_t qd = me + de + x, qs = qd - eff;
-                        const bool rd = !pc || bits_all(B, qs, 16);
-                        const u32x4 v = lds_ld16a(OUT + (pc ? qs : 0));
-                        if (__ballot(!rd) == 0) {
-                            if (pc) lds_put_al(OUT + qd, v, rem - x, MT);
+                        SrcRead rs;
+                        const int32_t qq = pc ? qs : 0;
+                        src_read(bbase + 4u * (uint32_t)(qq >> 5), obase + ((uint32_t)qq & ~7u), rs);
+                        const bool rdy = !pc || bits_in(rs.bits, qq & 31, 16);
+                        if (__ballot(!rdy) == 0) {
+                            if (pc) lds_put_ar(obase + (uint32_t)qd, funnel16(rs.w0, rs.w1, rs.w2, (uint32_t)qq & 7u), rem - x);
                             const int32_t wl = min(W, rem);
                             bits_fill_wave(B, me + de, wl, lane);
                             if ((int)lane == e) {
@@ -487,6 +547,13 @@ __global__ __launch_bounds__(kResT, 2) void res_exec_kernel(const uint8_t* __res
                     }
                 }
                 RS_MARK(5);
+                // ---- the chunk two ahead: its input positions and bytes.  Issued
+                // after the match loop, so that no load is in flight while it
+                // runs (a wait for any register a pending load targets would
+                // wait for it and every older load)
+                prepare(c + 2 * kResW, Lu, Q.t, Q.clen, Q.a, Q.b);
+                Ll = lens_at(c + 3 * kResW);
+                RS_MARK(4);
             };
             for (int32_t c = (int32_t)wv; c < nch; c += 3 * kResW) {
                 iter(c, S0, S2, L2, L0);

@@ -779,15 +779,33 @@ __device__ __forceinline__ int32_t next_base(int32_t op, int32_t base) {
     return op - base > kRowsH - kRowsRoom ? ((op - kRowsKeep) & ~15) : base;
 }
 
+// LZ4M_ROWS_NT: the compressed input and the length bytes are streamed (each
+// line read by one row, in order) -- non-temporal loads, so that they do not
+// push the blocks' recently flushed output (the far match sources) out of L2
+#ifndef LZ4M_ROWS_NT
+#define LZ4M_ROWS_NT 0
+#endif
+typedef u32x4 u32x4_u __attribute__((aligned(1)));
+__device__ __forceinline__ u32x4 ld16s(const uint8_t* p) {
+#if LZ4M_ROWS_NT
+    return __builtin_nontemporal_load((const u32x4_u*)p);
+#else
+    return ld16(p);
+#endif
+}
 // the round's inputs: 32 bytes at t (clamped into the block) and a length byte
 __device__ __forceinline__ void load_in(const uint8_t* s, int32_t t, int32_t iend, u32x4& a, u32x4& b) {
     const int32_t ta = t + 16 <= iend ? t : 0;   // good sequences: t + 16 < iend
     const int32_t tb = t + 32 <= iend ? t + 16 : iend - 16;
-    a = ld16(s + ta);
-    b = ld16(s + tb);
+    a = ld16s(s + ta);
+    b = ld16s(s + tb);
 }
 __device__ __forceinline__ int32_t load_len(const uint8_t* dl, int32_t k, int32_t nseq) {
+#if LZ4M_ROWS_NT
+    const int32_t v = (int32_t)__builtin_nontemporal_load(dl + (k < nseq ? k : nseq - 1));
+#else
     const int32_t v = (int32_t)dl[k < nseq ? k : nseq - 1];
+#endif
     return k < nseq ? v : 0;
 }
 

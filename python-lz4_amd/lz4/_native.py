@@ -12,6 +12,7 @@ from __future__ import annotations
 import collections
 import ctypes as C
 import os
+import sys
 import threading
 
 import torch
@@ -75,6 +76,7 @@ def _declare(lib) -> None:
         "lz4m_xxh32_host_update": ([vp, vp, C.c_size_t], None),
         "lz4m_xxh32_host_digest": ([vp], u32),
         "lz4m_xxh32_host": ([vp, C.c_size_t, u32], u32),
+        "lz4m_host_copy": ([vp, vp, C.c_size_t, i32, vp], None),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)
@@ -389,22 +391,121 @@ def xxh32_of_device(t: torch.Tensor, n: int, seed: int = 0, wait_stream=None, ch
 
 
 # ------------------------------------------------------------ host <-> device
+# Large host <-> device moves (the drop-in frame calls on Python bytes) go
+# through two pinned chunks: lz4m_host_copy fills / drains a chunk with a few
+# host threads while the other chunk's DMA runs on a side stream; a content
+# checksum can ride along (hashed from the chunk while it is copied).
+_BIG = 32 << 20
+_CHUNK = 64 << 20
+
+
+def _copy_threads() -> int:
+    try:
+        vis = len(os.sched_getaffinity(0))
+    except AttributeError:
+        vis = os.cpu_count() or 1
+    share = int(os.environ.get("OMP_NUM_THREADS", "16") or 16)
+    return max(1, min(8, vis, share) - 1)   # one core left for the hash thread
+
+
 def to_device(buf, dev=None, pad: int = 0) -> torch.Tensor:
     """Copy a bytes-like object to a device uint8 tensor (+pad zero bytes)."""
     dev = dev or device()
     mv = memoryview(buf).cast("B")
     n = mv.nbytes
     out = torch.empty(n + pad, dtype=torch.uint8, device=dev)
-    if n:
-        host = torch.frombuffer(bytearray(mv) if mv.readonly else mv, dtype=torch.uint8)
+    if n >= _BIG:
+        src, _, keep = _addr(mv)
+        bufs = _pinned_pair(_CHUNK)
+        evs = [None, None]
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        thr = _copy_threads()
+        try:
+            for i, lo in enumerate(range(0, n, _CHUNK)):
+                hi = min(n, lo + _CHUNK)
+                b = bufs[i & 1]
+                if evs[i & 1] is not None:
+                    evs[i & 1].synchronize()   # this chunk's previous DMA has read it
+                lib().lz4m_host_copy(b.data_ptr(), src + lo, hi - lo, thr, None)
+                with torch.cuda.stream(side):
+                    out[lo:hi].copy_(b[: hi - lo], non_blocking=True)
+                    evs[i & 1] = torch.cuda.Event()
+                    evs[i & 1].record(side)
+            torch.cuda.current_stream(dev).wait_stream(side)
+        finally:
+            for e in evs:
+                if e is not None:
+                    e.synchronize()
+            _pinned_release(_CHUNK, bufs)
+            del keep
+    elif n:
+        import warnings
+        with warnings.catch_warnings():   # read-only bytes: shared, only read
+            warnings.simplefilter("ignore")
+            host = torch.frombuffer(mv, dtype=torch.uint8)
         out[:n].copy_(host, non_blocking=False)
     if pad:
         out[n:].zero_()
     return out
 
 
-def to_host_bytes(t: torch.Tensor, n: int, as_bytearray: bool = False):
-    if n == 0:
-        return bytearray() if as_bytearray else b""
-    h = t[:n].cpu().numpy()
-    return bytearray(h.tobytes()) if as_bytearray else h.tobytes()
+_PyBytes_New = C.pythonapi.PyBytes_FromStringAndSize
+_PyBytes_New.restype = C.py_object
+_PyBytes_New.argtypes = [C.c_void_p, C.c_ssize_t]
+_PyByteArray_New = C.pythonapi.PyByteArray_FromStringAndSize
+_PyByteArray_New.restype = C.py_object
+_PyByteArray_New.argtypes = [C.c_void_p, C.c_ssize_t]
+_BYTES_DATA = sys.getsizeof(b"") - 1   # offset of a bytes object's data (CPython: the header, then the bytes)
+
+
+def _new_host_buffer(n: int, as_bytearray: bool):
+    """An uninitialised bytes (or bytearray) of n bytes and its data address
+    (filled before anyone else sees it)."""
+    if as_bytearray:
+        ba = _PyByteArray_New(None, n)
+        return ba, C.addressof((C.c_char * n).from_buffer(ba))
+    b = _PyBytes_New(None, n)
+    return b, id(b) + _BYTES_DATA
+
+
+def to_host_bytes(t: torch.Tensor, n: int, as_bytearray: bool = False, hash_seed: int | None = None):
+    """The first n bytes of a device tensor as a new bytes (or bytearray).
+    hash_seed: also return the XXH32 of those bytes, hashed on a host core
+    from each staged chunk while it is copied -> (bytes, digest)."""
+    if n <= 0:
+        out = bytearray() if as_bytearray else b""
+        return (out, HostXXH32(hash_seed).digest()) if hash_seed is not None else out
+    if n < _BIG:
+        h = t.view(-1)[:n].cpu().numpy()
+        out = bytearray(h.tobytes()) if as_bytearray else h.tobytes()
+        return (out, xxh32_host(out, hash_seed)) if hash_seed is not None else out
+    out, dst = _new_host_buffer(n, as_bytearray)
+    st = HostXXH32(hash_seed) if hash_seed is not None else None
+    dev = t.device
+    flat = t.view(-1)
+    side = torch.cuda.Stream(dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    bufs = _pinned_pair(_CHUNK)
+    evs = [torch.cuda.Event(), torch.cuda.Event()]
+    spans = [(lo, min(n, lo + _CHUNK)) for lo in range(0, n, _CHUNK)]
+    thr = _copy_threads()
+
+    def issue(i):
+        lo, hi = spans[i]
+        with torch.cuda.stream(side):
+            bufs[i & 1][: hi - lo].copy_(flat[lo:hi], non_blocking=True)
+            evs[i & 1].record(side)
+
+    try:
+        issue(0)
+        for i, (lo, hi) in enumerate(spans):
+            if i + 1 < len(spans):
+                issue(i + 1)   # its buffer was drained in iteration i - 1
+            evs[i & 1].synchronize()
+            lib().lz4m_host_copy(dst + lo, bufs[i & 1].data_ptr(), hi - lo, thr, None if st is None else st._st)
+    finally:
+        for e in evs:
+            e.synchronize()
+        _pinned_release(_CHUNK, bufs)
+    return (out, st.digest()) if st is not None else out

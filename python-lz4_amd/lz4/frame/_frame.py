@@ -199,8 +199,7 @@ def compress(data, compression_level=0, block_size=0, content_checksum=False, bl
     frame = _compress_frame(d_src, src.nbytes, compression_level=level, block_size=bsid_req,
                             content_checksum=content_checksum, block_checksum=block_checksum,
                             block_linked=block_linked, store_size=store_size, host_src=src)[0]
-    out = frame.cpu().numpy().tobytes()
-    return bytearray(out) if return_bytearray else out
+    return N.to_host_bytes(frame, frame.numel(), bool(return_bytearray))
 
 
 def compress_device(d_src: torch.Tensor, n: int | None = None, *, compression_level=0, block_size=0,
@@ -389,10 +388,16 @@ def decompress(data, return_bytearray=False, return_bytes_read=False):
             t([r[0] for r in recs], torch.bool), t([r[3] for r in recs], torch.int64))
     _frame_errors(first_err, state, info, total)
     bytes_read = state[1]
-    out = N.to_host_bytes(out_t, total, bool(return_bytearray)) if total else (bytearray() if return_bytearray else b"")
-    if info["content_checksum"]:   # on the host copy the caller gets (lz4frame.c:1850, :1959-1964)
+    host_hash = info["content_checksum"] and not (total and _content_on_gpu())
+    got = None
+    if host_hash:   # on the copy the caller gets, hashed while it is staged (lz4frame.c:1850, :1959-1964)
+        out, got = N.to_host_bytes(out_t, total, bool(return_bytearray), hash_seed=0)
+    else:
+        out = N.to_host_bytes(out_t, total, bool(return_bytearray))
+    if info["content_checksum"]:
         want = struct.unpack_from("<I", mv, state[2])[0]
-        got = _xxh32_dev(out_t, total) if (total and _content_on_gpu()) else N.xxh32_host(out)
+        if got is None:
+            got = _xxh32_dev(out_t, total)
         if got != want:
             raise _err("LZ4F_decompress", "contentChecksum_invalid")
     if return_bytes_read:

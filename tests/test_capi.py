@@ -76,8 +76,8 @@ def test_argument_validation_without_gpu():
                                           N.LINKED_SPECULATIVE, None, 0, None) == N.EINVAL
     assert lib.lz4m_compress_linked_workspace_size(4) >= 4 * 2 * 16384
     assert lib.lz4m_xxh32_batch(None, None, None, 0, None, -1, None) == N.EINVAL
-    # retired decoder ids (1 lane, 2 coop, 5 direct) and unknown ids are rejected before any launch
-    for dec in (1, 2, 5, 7, -1):
+    # retired decoder ids (1 lane, 2 coop, 5 direct, 6) and unknown ids are rejected before any launch
+    for dec in (1, 2, 5, 6, 8, -1):
         assert lib.lz4m_decompress_batch_sel(None, None, None, None, None, None, None, 0, None, 0, dec,
                                              None) == N.EINVAL
     for dec in N.DECODERS.values():
