@@ -370,6 +370,15 @@ void lz4m_xxh32_host_update(lz4m_xxh32_state* state, const void* input, size_t l
 uint32_t lz4m_xxh32_host_digest(const lz4m_xxh32_state* state);
 uint32_t lz4m_xxh32_host(const void* input, size_t length, uint32_t seed);
 
+/* The single-call functions above (lz4m_decompress_safe*, lz4m_compress_*
+ * on blocks up to 64 KiB) are served by a persistent one-workgroup kernel per
+ * host thread and kind that polls a mailbox in mapped pinned memory, so a
+ * call while others keep coming pays no kernel launch; it exits after 2 ms
+ * without a call and is started again by the next one.  mode 1 = on (the
+ * default; env LZ4M_WORKER=0 turns it off), 0 = off (one launch of the
+ * lone-block kernel per call), -1 = query.  Returns the previous mode. */
+int lz4m_single_call_worker(int mode);
+
 /* Host memcpy of n bytes split over `threads` threads (1..16; one below
  * 4 MiB); when `hash` is not NULL, one more thread runs
  * lz4m_xxh32_host_update(hash, src, n) over the same source meanwhile.  The

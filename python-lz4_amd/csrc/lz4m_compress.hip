@@ -22,6 +22,7 @@
 // copies are coalesced 16-byte-per-lane copies; sequence headers are written
 // by lane 0.
 #include "lz4m_common.h"
+#include "lz4m_worker.h"
 
 #include <type_traits>
 
@@ -698,13 +699,10 @@ constexpr int kSoloMax = kLimit64K - 1;                  // the U16 table's rang
 constexpr int kSoloBuf = ((kSoloMax + 64) + 15) & ~15;   // + zero padding past the block
 constexpr int kSoloU = 4;   // 16-byte pieces in flight per lane when staging / copying out
 template <int V, bool ACC1>
-__global__ __launch_bounds__(256) void compress_solo_kernel(const uint8_t* __restrict__ src, int32_t len,
-                                                            uint8_t* dst, int32_t cap, int32_t* __restrict__ out_len,
-                                                            int accel, uint8_t* h_out, int32_t* h_done) {
-    __shared__ int32_t solo_r;
-    __shared__ __attribute__((aligned(16))) uint8_t blk[kSoloBuf];
-    __shared__ __attribute__((aligned(16))) uint16_t tab[8192];
-    RING_DECL
+__device__ __forceinline__ void compress_solo_body(const uint8_t* __restrict__ src, int32_t len, uint8_t* dst,
+                                                   int32_t cap, int32_t* __restrict__ out_len, int accel,
+                                                   uint8_t* h_out, int32_t* h_done, uint8_t* blk, uint16_t* tab,
+                                                   lds_u8* ring, int32_t& solo_r) {
     const uint32_t t = threadIdx.x;
     constexpr int kStep = 16 * 256;
     const int32_t lim = len + 64 < kSoloBuf ? len + 64 : kSoloBuf;   // the block and 64 zero bytes
@@ -949,9 +947,66 @@ __global__ __launch_bounds__(64) void compress_spec_kernel(
     }
 }
 
+
+// (the LDS buffers are the caller's: one set for the launch-per-call kernel,
+// one set shared by every table variant of the persistent worker)
+template <int V, bool ACC1>
+__global__ __launch_bounds__(256) void compress_solo_kernel(const uint8_t* __restrict__ src, int32_t len,
+                                                            uint8_t* dst, int32_t cap, int32_t* __restrict__ out_len,
+                                                            int accel, uint8_t* h_out, int32_t* h_done) {
+    __shared__ int32_t solo_r;
+    __shared__ __attribute__((aligned(16))) uint8_t blk[kSoloBuf];
+    __shared__ __attribute__((aligned(16))) uint16_t tab[8192];
+    RING_DECL
+    compress_solo_body<V, ACC1>(src, len, dst, cap, out_len, accel, h_out, h_done, blk, tab, ring, solo_r);
+}
+
+// The single-call compress worker (lz4m_worker.h): one persistent workgroup
+// serving lone-block compress requests from its mailbox with the solo body;
+// the LDS buffers are declared once here and shared by every table variant.
+__global__ __launch_bounds__(256) void compress_worker(Mailbox* mb, uint8_t* hd, uint8_t* dbuf, uint64_t idle) {
+    __shared__ uint32_t cmd[8];
+    __shared__ int32_t solo_r;
+    __shared__ __attribute__((aligned(16))) uint8_t blk[kSoloBuf];
+    __shared__ __attribute__((aligned(16))) uint16_t tab[8192];
+    RING_DECL
+    uint32_t last = worker_init(mb, cmd);
+    for (;;) {
+        if (worker_next(mb, last, idle, cmd) == 0) break;
+        const int32_t rec_off = (int32_t)cmd[1], len = (int32_t)cmd[2], cap = (int32_t)cmd[3];
+        const int table = (int)cmd[4];
+        int accel = (int)cmd[5];
+        if (accel < 1) accel = 1;   // lz4.c:1350-1351
+        if (accel > 65537) accel = 65537;
+        CallMeta* rec = reinterpret_cast<CallMeta*>(hd + rec_off);
+        uint8_t* hout = hd + rec_off + kCallMeta;
+        if (table == LZ4M_TABLE_U32_HASH5) {
+            if (accel == 1)
+                compress_solo_body<LZ4M_TABLE_U32_HASH5, true>(hd, len, dbuf, cap, &rec->result, accel, hout, &rec->done,
+                                                              blk, tab, ring, solo_r);
+            else
+                compress_solo_body<LZ4M_TABLE_U32_HASH5, false>(hd, len, dbuf, cap, &rec->result, accel, hout,
+                                                               &rec->done, blk, tab, ring, solo_r);
+        } else {   // AUTO / U16: below 65547 bytes the byU16 parse (lz4.c:1352-1357)
+            if (accel == 1)
+                compress_solo_body<LZ4M_TABLE_U16_HASH4, true>(hd, len, dbuf, cap, &rec->result, accel, hout, &rec->done,
+                                                              blk, tab, ring, solo_r);
+            else
+                compress_solo_body<LZ4M_TABLE_U16_HASH4, false>(hd, len, dbuf, cap, &rec->result, accel, hout,
+                                                               &rec->done, blk, tab, ring, solo_r);
+        }
+    }
+}
+
 }  // namespace lz4m
 
 using namespace lz4m;
+
+extern "C" int lz4m_compress_worker_launch(Mailbox* mb, uint8_t* hd, uint8_t* dbuf, uint64_t idle_ticks,
+                                           hipStream_t stream) {
+    hipLaunchKernelGGL(compress_worker, dim3(1), dim3(256), 0, stream, mb, hd, dbuf, idle_ticks);
+    return (int)hipGetLastError();
+}
 
 extern "C" int lz4m_compress_bound(int input_size) {
     if ((unsigned)input_size > (unsigned)kMaxInput) return 0;

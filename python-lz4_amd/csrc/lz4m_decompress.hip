@@ -22,6 +22,7 @@
 // compressed size + decoded size.
 #include "lz4m_common.h"
 #include "lz4m_rows.h"
+#include "lz4m_worker.h"
 #include "../../include/lz4m.h"
 
 #include <stdlib.h>
@@ -820,14 +821,14 @@ __device__ unsigned long long g_hist_prof[16];
 constexpr int32_t kSoloIn = 66 * 1024;   // > LZ4_compressBound(65536) + 64
 constexpr int kSoloU = 4;               // 16-byte pieces in flight per lane when staging / copying out
 template <bool DICT, bool SOLO = false>
-__global__ __launch_bounds__(256, 4) void hist_decompress_kernel(const uint8_t* __restrict__ src,
-                                                                 const int64_t* __restrict__ src_off,
-                                                                 const int32_t* __restrict__ src_len, uint8_t* dst,
-                                                                 const int64_t* __restrict__ dst_off,
-                                                                 const int32_t* __restrict__ dst_cap,
-                                                                 int32_t* __restrict__ status, int64_t n,
-                                                                 const int32_t* __restrict__ dict_len, int64_t ddelta,
-                                                                 uint8_t* solo_out, int32_t* solo_done) {
+__device__ __forceinline__ void hist_decompress_body(const uint8_t* __restrict__ src,
+                                                     const int64_t* __restrict__ src_off,
+                                                     const int32_t* __restrict__ src_len, uint8_t* dst,
+                                                     const int64_t* __restrict__ dst_off,
+                                                     const int32_t* __restrict__ dst_cap,
+                                                     int32_t* __restrict__ status, int64_t n,
+                                                     const int32_t* __restrict__ dict_len, int64_t ddelta,
+                                                     uint8_t* solo_out, int32_t* solo_done) {
     __shared__ __attribute__((aligned(16))) uint8_t ins[4][kCoopIn + 64];
     __shared__ __attribute__((aligned(16))) uint8_t outs[4][kHistW + 32];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -1134,6 +1135,39 @@ __global__ __launch_bounds__(256, 4) void hist_decompress_kernel(const uint8_t* 
 #undef HLD
 }
 
+// (the body is shared with the single-call worker, lz4m_worker.hip)
+template <bool DICT, bool SOLO = false>
+__global__ __launch_bounds__(256, 4) void hist_decompress_kernel(const uint8_t* __restrict__ src,
+                                                                 const int64_t* __restrict__ src_off,
+                                                                 const int32_t* __restrict__ src_len, uint8_t* dst,
+                                                                 const int64_t* __restrict__ dst_off,
+                                                                 const int32_t* __restrict__ dst_cap,
+                                                                 int32_t* __restrict__ status, int64_t n,
+                                                                 const int32_t* __restrict__ dict_len, int64_t ddelta,
+                                                                 uint8_t* solo_out, int32_t* solo_done) {
+    hist_decompress_body<DICT, SOLO>(src, src_off, src_len, dst, dst_off, dst_cap, status, n, dict_len, ddelta,
+                                     solo_out, solo_done);
+}
+
+// The single-call decompress worker: one persistent workgroup that serves
+// the lone-block requests of one host thread from its mailbox with the
+// SOLO body above (input and record read from mapped pinned memory, output
+// written back into it, done flag released), until told to quit or idle.
+__global__ __launch_bounds__(256) void decompress_worker(Mailbox* mb, uint8_t* hd, uint8_t* dbuf, uint64_t idle) {
+    __shared__ uint32_t cmd[8];
+    __shared__ int64_t zero_off;   // the record's offsets and sizes, read by the body from LDS, not over PCIe
+    uint32_t last = worker_init(mb, cmd);
+    if (threadIdx.x == 0) zero_off = 0;
+    for (;;) {
+        if (worker_next(mb, last, idle, cmd) == 0) break;
+        const int32_t rec_off = (int32_t)cmd[1];
+        CallMeta* rec = reinterpret_cast<CallMeta*>(hd + rec_off);
+        const int32_t* len_cap = reinterpret_cast<const int32_t*>(cmd + 2);   // cmd[2] = src_len, cmd[3] = dst_cap
+        hist_decompress_body<false, true>(hd, &zero_off, len_cap, dbuf, &zero_off, len_cap + 1, &rec->result,
+                                          (int64_t)1, nullptr, (int64_t)0, hd + rec_off + kCallMeta, &rec->done);
+    }
+}
+
 // Linked-block frames (lz4frame.c:1853-1856, LZ4F_updateDict): block i may
 // reference the output of blocks < i, so the chain decodes in order on one
 // wavefront, contiguously into dst.  Lane 0 parses; the wave runs the long
@@ -1308,6 +1342,14 @@ extern "C" int lz4m_decompress_solo(const uint8_t* d_src, const int64_t* d_src_o
     if (src_len_host < 0 || src_len_host > kSoloIn - 64) return LZ4M_EINVAL;
     hipLaunchKernelGGL((hist_decompress_kernel<false, true>), dim3(1), dim3(256), 0, (hipStream_t)stream, d_src,
                        d_src_off, d_src_len, d_dst, d_dst_off, d_dst_cap, d_status, (int64_t)1, nullptr, (int64_t)0, h_out, h_done);
+    return (int)hipGetLastError();
+}
+
+extern "C" int lz4m_worker_launch(int kind, Mailbox* mb, uint8_t* hd, uint8_t* dbuf, uint64_t idle_ticks,
+                                  hipStream_t stream) {
+    if (kind == 1) return lz4m_compress_worker_launch(mb, hd, dbuf, idle_ticks, stream);
+    if (kind != 0) return LZ4M_EINVAL;
+    hipLaunchKernelGGL(decompress_worker, dim3(1), dim3(256), 0, stream, mb, hd, dbuf, idle_ticks);
     return (int)hipGetLastError();
 }
 

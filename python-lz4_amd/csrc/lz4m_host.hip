@@ -10,10 +10,15 @@
 // back; device buffers are cached per thread and grow as needed.  Throughput
 // comes from the batched entry points.
 #include "../../include/lz4m.h"
+#include "lz4m_worker.h"
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
+
+#include <atomic>
+#include <chrono>
 
 namespace {
 
@@ -70,12 +75,8 @@ thread_local const uint8_t* t_out = nullptr;   // the last call's output in the 
 
 inline size_t up(size_t x) { return (x + 255) & ~(size_t)255; }
 
-struct CMeta {
-    int64_t src_off, dst_off;
-    int32_t src_len, dst_cap, result, done;   // done: set by a lone-block kernel when its output is in host memory
-    uint64_t work[8];   // decoder scratch (lz4m_decompress_workspace_bytes)
-};
-static_assert(sizeof(CMeta) <= kMeta, "record size");
+typedef lz4m::CallMeta CMeta;   // the call record (lz4m_worker.h), shared with the single-call workers
+static_assert(sizeof(CMeta) <= kMeta && kMeta == lz4m::kCallMeta, "record size");
 
 // One block through a batched entry point.  Layout (device and pinned host
 // alike): [input, up(len)] [record, kMeta] [output, cap]; copies in the first
@@ -135,11 +136,16 @@ int32_t one_block_mapped(const char* src, int32_t len, char* dst, int32_t cap, i
     // output: poll it (the completion signal and the waiting thread's wake-up
     // cost ~10 us more); every 256 polls check the stream, so a failed launch
     // ends the wait
+    const auto t0 = std::chrono::steady_clock::now();
     for (uint32_t i = 1; __atomic_load_n(&hm->done, __ATOMIC_ACQUIRE) == 0; ++i) {
         if ((i & 255) == 0) {
             const hipError_t q = hipStreamQuery(s);
             if (q == hipSuccess && __atomic_load_n(&hm->done, __ATOMIC_ACQUIRE) == 0) return fail;   // ended without the flag
             if (q != hipSuccess && q != hipErrorNotReady) return fail;
+            // a lone block takes well under a millisecond: a kernel that has
+            // not finished in 30 s is queued behind something that does not
+            // end, and the call fails instead of waiting without bound
+            if ((i & 0xFFFF) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(30)) return fail;
         }
         __builtin_ia32_pause();
     }
@@ -149,6 +155,171 @@ int32_t one_block_mapped(const char* src, int32_t len, char* dst, int32_t cap, i
     return m.result;
 }
 
+// ---------------------------------------------------- single-call workers
+// A lone call served by a persistent one-workgroup kernel that polls a
+// mailbox in mapped pinned memory (lz4m_worker.h): while calls keep coming,
+// none of them pays a kernel launch.  One worker per kind (decompress /
+// compress) and host thread; it exits by itself after kIdle of no requests
+// (so a stream it shares a hardware queue with waits at most that long), on
+// the host's quit, or when the thread ends.  A call whose worker has exited
+// starts it again; calls outside its buffers take the launch-per-call path.
+constexpr size_t kWorkIn = 66 * 1024;         // input region: the lone-block kernels' ranges
+constexpr size_t kWorkOut = 1 << 20;          // output region: capacities up to 1 MiB
+constexpr size_t kWorkMb = 128;               // two mailboxes
+constexpr uint64_t kIdle = 200000;            // 2 ms of the 100 MHz real-time clock
+
+std::atomic<int> g_worker_mode{-1};           // -1: from LZ4M_WORKER at first use
+std::atomic<int> g_worker_failures{0};        // requests a worker neither served nor gave up within 1 s
+bool worker_enabled() {
+    int m = g_worker_mode.load(std::memory_order_relaxed);
+    if (m < 0) {
+        const char* e = getenv("LZ4M_WORKER");
+        m = (e != nullptr && e[0] == '0') ? 0 : 1;
+        g_worker_mode.store(m, std::memory_order_relaxed);
+    }
+    return m != 0;
+}
+
+struct Workers {
+    int dev = -1;
+    uint8_t* host = nullptr;       // [mailbox 0 | mailbox 1] then per kind [input kWorkIn] [record kMeta] [output kWorkOut]
+    uint8_t* host_dev = nullptr;
+    uint8_t* dbuf = nullptr;       // device output buffers, one per kind
+    hipStream_t stream[2] = {nullptr, nullptr};
+    bool launched[2] = {false, false};
+    uint32_t seq[2] = {0, 0};
+    lz4m::Mailbox* mb(int k) { return reinterpret_cast<lz4m::Mailbox*>(host + 64 * k); }
+    static constexpr size_t kRegion = kWorkIn + kMeta + kWorkOut + 256;
+    size_t region(int k) const { return kWorkMb + (size_t)k * kRegion; }
+    uint8_t* base(int k) { return host + region(k); }
+    bool idle(int k) { return hipStreamQuery(stream[k]) == hipSuccess; }
+    void stop(int k) {
+        if (!launched[k]) return;
+        __atomic_store_n(&mb(k)->quit, 1u, __ATOMIC_RELEASE);
+        const auto t0 = std::chrono::steady_clock::now();
+        while (hipStreamQuery(stream[k]) == hipErrorNotReady &&
+               std::chrono::steady_clock::now() - t0 < std::chrono::seconds(2))
+            __builtin_ia32_pause();
+        launched[k] = false;
+        __atomic_store_n(&mb(k)->quit, 0u, __ATOMIC_RELEASE);
+    }
+    void release() {
+        for (int k = 0; k < 2; ++k) stop(k);
+        for (int k = 0; k < 2; ++k)
+            if (stream[k]) (void)hipStreamDestroy(stream[k]);
+        if (dbuf) (void)hipFree(dbuf);
+        if (host) (void)hipHostFree(host);
+        host = host_dev = dbuf = nullptr;
+        stream[0] = stream[1] = nullptr;
+    }
+    ~Workers() { release(); }
+    bool get() {
+        int d = 0;
+        if (hipGetDevice(&d) != hipSuccess) return false;
+        if (d != dev) {
+            release();
+            dev = d;
+        }
+        if (host) return true;
+        const size_t bytes = kWorkMb + 2 * kRegion;
+        // coherent (fine-grained): the worker reads the mailbox and each request's bytes
+        // while it runs, with no kernel boundary to invalidate a cached copy
+        if (hipHostMalloc(reinterpret_cast<void**>(&host), bytes, hipHostMallocMapped | hipHostMallocCoherent) !=
+            hipSuccess)
+            return false;
+        memset(host, 0, kWorkMb);
+        if (hipHostGetDevicePointer(reinterpret_cast<void**>(&host_dev), host, 0) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void**>(&dbuf), 2 * (kWorkOut + 256)) != hipSuccess) {
+            release();
+            return false;
+        }
+        for (int k = 0; k < 2; ++k)
+            if (hipStreamCreateWithFlags(&stream[k], hipStreamNonBlocking) != hipSuccess) {
+                release();
+                return false;
+            }
+        return true;
+    }
+    bool start(int k) {
+        if (launched[k] && idle(k)) launched[k] = false;   // exited (idle or quit)
+        if (launched[k]) return true;
+        __atomic_store_n(&mb(k)->quit, 0u, __ATOMIC_RELEASE);
+        if (lz4m_worker_launch(k, reinterpret_cast<lz4m::Mailbox*>(host_dev + 64 * k), host_dev + region(k),
+                               dbuf + (size_t)k * (kWorkOut + 256), kIdle, stream[k]) != 0)
+            return false;
+        launched[k] = true;
+        return true;
+    }
+};
+thread_local Workers t_workers;
+
+// One block through the thread's worker of `kind` (0 decompress, 1 compress).
+// Returns false (nothing done) when the worker path does not apply.
+bool one_block_worker(int kind, const char* src, int32_t len, char* dst, int32_t cap, int32_t fail, int table,
+                      int accel, int32_t* result) {
+    if (!worker_enabled()) return false;
+    const size_t in = up((size_t)len + 16);
+    const int32_t out_cap = kind == 1 ? lz4m_compress_bound(len) : cap;
+    if (in > kWorkIn || out_cap > (int32_t)kWorkOut || len < 0) return false;
+    Workers& W = t_workers;
+    if (!W.get()) return false;
+    uint8_t* h = W.base(kind);
+    if (len) memcpy(h, src, (size_t)len);
+    CMeta m{};
+    m.src_off = 0;
+    m.dst_off = 0;   // output at the device buffer's start
+    m.src_len = len;
+    m.dst_cap = cap;
+    m.result = fail;
+    memcpy(h + in, &m, sizeof m);
+    lz4m::Mailbox* M = W.mb(kind);
+    M->rec_off = (int32_t)in;
+    M->src_len = len;
+    M->dst_cap = cap;
+    M->table = table;
+    M->accel = accel;
+    if (!W.start(kind)) return false;
+    if (++W.seq[kind] == 0) W.seq[kind] = 1;
+    __atomic_store_n(&M->seq, W.seq[kind], __ATOMIC_RELEASE);
+    CMeta* hm = reinterpret_cast<CMeta*>(h + in);
+    int restarts = 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    // every 256 polls: has the worker exited without serving (it went idle
+    // as the request arrived)?  Then start it again; it serves the request.
+    // A worker that neither serves nor exits within a second is stopped and
+    // the worker path is turned off for the process (the launch path then
+    // serves every call): a call never waits on it without bound.
+    for (uint32_t i = 1; __atomic_load_n(&hm->done, __ATOMIC_ACQUIRE) == 0; ++i) {
+        if ((i & 255) == 0) {
+            const hipError_t q = hipStreamQuery(W.stream[kind]);
+            if (__atomic_load_n(&hm->done, __ATOMIC_ACQUIRE) != 0) break;
+            if (q != hipSuccess && q != hipErrorNotReady) {
+                g_worker_mode.store(0, std::memory_order_relaxed);
+                return false;
+            }
+            if (q == hipSuccess) {
+                if (++restarts > 3) {
+                    g_worker_mode.store(0, std::memory_order_relaxed);
+                    return false;
+                }
+                W.launched[kind] = false;
+                if (!W.start(kind)) return false;
+            } else if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(1)) {
+                g_worker_failures.fetch_add(1, std::memory_order_relaxed);
+                g_worker_mode.store(0, std::memory_order_relaxed);
+                W.stop(kind);
+                return false;
+            }
+        }
+        __builtin_ia32_pause();
+    }
+    memcpy(&m, h + in, sizeof m);
+    t_out = h + in + kMeta;
+    if (dst && m.result > 0 && m.result <= cap) memcpy(dst, h + in + kMeta, (size_t)m.result);
+    *result = m.result;
+    return true;
+}
+
 // one-block compress through the batched compressors; returns the compressed size or 0
 // dst == nullptr: the output stays in the pinned buffer (t_out), for the _staged calls
 int compress_one(const char* src, char* dst, int srcSize, int dstCapacity, int table, int acceleration) {
@@ -156,6 +327,8 @@ int compress_one(const char* src, char* dst, int srcSize, int dstCapacity, int t
     // blocks below 65547 bytes: the LDS-staged lone-block kernel (the
     // skip-ahead search then waits on no memory round trip), no copies
     if (srcSize < kSoloLimit) {
+        int32_t rw = 0;
+        if (one_block_worker(1, src, srcSize, dst, dstCapacity, 0, table, acceleration, &rw)) return rw > 0 ? rw : 0;
         const int32_t r = one_block_mapped(
             src, srcSize, dst, dstCapacity, 0, [&](uint8_t* hd, CMeta* hm, uint8_t* d, uint8_t* hout, hipStream_t s) {
                 return lz4m_compress_solo(hd, srcSize, d, dstCapacity, &hm->result, table, acceleration, hout,
@@ -174,6 +347,9 @@ int compress_one(const char* src, char* dst, int srcSize, int dstCapacity, int t
 int decompress_one(const char* src, char* dst, int compressedSize, int dstCapacity) {
     // inputs up to 66 KiB - 64 (any 64 KiB block): the LDS-staged lone-block
     // decoder, no copies
+    int32_t rw = 0;
+    if (compressedSize <= kSoloDecIn && one_block_worker(0, src, compressedSize, dst, dstCapacity, -1, 0, 1, &rw))
+        return rw;
     if (compressedSize <= kSoloDecIn)
         return one_block_mapped(src, compressedSize, dst, dstCapacity, -1,
                                 [&](uint8_t* hd, CMeta* hm, uint8_t* d, uint8_t* hout, hipStream_t s) {
@@ -222,6 +398,37 @@ extern "C" int lz4m_compress_block_api_staged(const char* src, int srcSize, int 
     }
     *out = reinterpret_cast<const char*>(t_out) - header;
     return r;
+}
+
+// diagnostics (tests, probes): out[0..7] = this thread's decompress / compress
+// mailbox seq, served, quit, and the launched flags; out[8..11] = per kind the
+// requests its last launch served and how that launch ended (1 idle, 2 quit);
+// returns the failure count
+extern "C" int lz4m_single_call_worker_state(uint32_t* out) {
+    Workers& W = t_workers;
+    for (int k = 0; k < 2; ++k) {
+        lz4m::Mailbox* M = W.host ? W.mb(k) : nullptr;
+        out[3 * k] = M ? __atomic_load_n(&M->seq, __ATOMIC_ACQUIRE) : 0u;
+        out[3 * k + 1] = M ? __atomic_load_n(&M->served, __ATOMIC_ACQUIRE) : 0u;
+        out[3 * k + 2] = M ? __atomic_load_n(&M->quit, __ATOMIC_ACQUIRE) : 0u;
+        out[8 + 2 * k] = M ? __atomic_load_n(&M->pad[0], __ATOMIC_ACQUIRE) : 0u;
+        out[9 + 2 * k] = M ? __atomic_load_n(&M->pad[1], __ATOMIC_ACQUIRE) : 0u;
+    }
+    out[6] = W.launched[0];
+    out[7] = W.launched[1];
+    return g_worker_failures.load(std::memory_order_relaxed);
+}
+
+extern "C" int lz4m_single_call_worker(int mode) {
+    const int prev = worker_enabled() ? 1 : 0;
+    if (mode == 0 || mode == 1) {
+        g_worker_mode.store(mode, std::memory_order_relaxed);
+        if (mode == 0) {   // this thread's workers stop now (other threads' go idle by themselves)
+            t_workers.stop(0);
+            t_workers.stop(1);
+        }
+    }
+    return prev;
 }
 
 extern "C" uint32_t lz4m_xxh32(const void* input, size_t length, uint32_t seed) {

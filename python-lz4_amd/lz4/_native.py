@@ -77,6 +77,8 @@ def _declare(lib) -> None:
         "lz4m_xxh32_host_digest": ([vp], u32),
         "lz4m_xxh32_host": ([vp, C.c_size_t, u32], u32),
         "lz4m_host_copy": ([vp, vp, C.c_size_t, i32, vp], None),
+        "lz4m_single_call_worker": ([i32], i32),
+        "lz4m_single_call_worker_state": ([vp], i32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)

@@ -600,13 +600,25 @@ def test_decompress_host_pipelined(gpu):
             assert out[o:o + want].numpy().tobytes() == data[:want], i
 
 
+@pytest.fixture(params=[1, 0], ids=["worker", "launch"])
+def single_call_mode(request):
+    """The single-call functions served by the persistent worker (default)
+    and by one launch of the lone-block kernel per call (its fallback)."""
+    import lz4._native as N
+    lib = N.lib()
+    prev = lib.lz4m_single_call_worker(request.param)
+    yield request.param
+    lib.lz4m_single_call_worker(prev)
+
+
 @pytest.mark.parametrize("kind", ["random", "text", "runs", "zeros"])
-def test_single_call_compress_vs_oracle(gpu, oracle, kind):
+def test_single_call_compress_vs_oracle(gpu, oracle, kind, single_call_mode):
     """lz4m_compress_default / lz4m_compress_block_api (the single-call entry
     points, include/lz4m.h) against the oracle at sizes on both sides of the
     LDS-staged lone-block kernel's limit (lz4m_compress_solo: < 65547 bytes,
     LZ4_64Klimit, lz4.c:689), with full and limited output capacity and
-    accelerations 1 and 7."""
+    accelerations 1 and 7; served by the persistent worker and by one launch
+    per call."""
     import ctypes as C
     import lz4._native as N
     from oracle import TABLE_U32_HASH5, compress_bound
@@ -640,7 +652,7 @@ def test_single_call_compress_vs_oracle(gpu, oracle, kind):
                     assert (dst.raw[:got] if got > 0 else None) == want, (kind, n, cap, "default")
 
 
-def test_single_call_decompress_golden_and_mutated(gpu, golden, oracle):
+def test_single_call_decompress_golden_and_mutated(gpu, golden, oracle, single_call_mode):
     """lz4m_decompress_safe (single call; inputs <= 66 KiB - 64 run the
     LDS-staged lone-block decoder, lz4m_decompress_solo) returns the
     reference's status for every golden decompress case (statuses from the

@@ -16,10 +16,9 @@ while read -r grp; do
   i=$((i+1))
   timeout -k 10 420 rocprofv3 --kernel-include-regex "$KRX" --pmc $grp -d "$OUT/p$i" -o p$i --output-format csv -- python3 "$REPO/bench.py" $ARGS > "$OUT/p$i.log" 2>&1
   echo "pass $i done: $grp"
-done <<'GROUPS'
+done <<GROUPS
 FETCH_SIZE
 WRITE_SIZE
-TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum
-TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum TCC_EA0_RDREQ_DRAM_sum TCC_HIT_sum
+${PMC_QUICK:+}$( [ -z "$PMC_QUICK" ] && printf '%s\n%s' "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum" "TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum TCC_EA0_RDREQ_DRAM_sum TCC_HIT_sum" || true )
 GROUPS
 python3 "$REPO/tools/pmc_report.py" "$OUT" "$OUT/pmc_decompress.json" 1048576 4096 "${CAL:-}" > "$OUT/report.json"

@@ -13,11 +13,10 @@ import collections
 import csv
 import glob
 import json
+import os
 import sys
 
-import os
-
-KERNELS = ("rows_parse_kernel", "rows_exec_kernel", "decompress_kernel<false, true>")
+KERNELS = tuple(os.environ.get("PMC_KERNELS", "rows_parse_kernel,rows_exec_kernel,decompress_kernel<false, true>").split(","))
 d = sys.argv[1]
 per = collections.defaultdict(dict)   # launch order -> counter -> value
 for f in sorted(glob.glob(f"{d}/p*/p*_counter_collection.csv")):
