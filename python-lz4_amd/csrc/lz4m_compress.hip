@@ -691,21 +691,28 @@ __global__ __launch_bounds__(64) void compress_kernel(const uint8_t* __restrict_
 // One lone block of < 65547 bytes (the single-call API, lz4m_host.hip): the
 // workgroup's four waves stage the whole block in LDS, then wave 0 runs the
 // same parse with every source read -- hash inputs, candidates, catch-up,
-// match extension, literals -- from LDS instead of L2/HBM.  A lone block is
-// latency-bound (the skip-ahead search waits one memory round trip per 64
-// attempts); occupancy does not matter for a batch of one, so 64 KiB of LDS
-// per workgroup is free here.  Output bytes are the batched kernel's.
+// match extension, literals -- from LDS instead of L2/HBM, and writes the
+// compressed block into LDS too, so no memory operation of the parse waits
+// for a store to reach L2.  A lone block is latency-bound (the skip-ahead
+// search waits one round trip per 64 attempts); occupancy does not matter for
+// a batch of one, so ~150 KiB of LDS per workgroup is free here.  Output
+// bytes are the batched kernel's.
 constexpr int kSoloMax = kLimit64K - 1;                  // the U16 table's range (lz4.c:1352)
 constexpr int kSoloBuf = ((kSoloMax + 64) + 15) & ~15;   // + zero padding past the block
-constexpr int kSoloU = 4;   // 16-byte pieces in flight per lane when staging / copying out
+constexpr int kSoloBound = kSoloMax + kSoloMax / 255 + 16;          // LZ4_compressBound(kSoloMax)
+constexpr int kSoloOut = ((kSoloBound + 15) & ~15) + 64;            // + room for 16-byte wild stores
+constexpr int kSoloU = 4;   // 16-byte pieces in flight per lane when staging
 template <int V, bool ACC1>
 __device__ __forceinline__ void compress_solo_body(const uint8_t* __restrict__ src, int32_t len, uint8_t* dst,
                                                    int32_t cap, int32_t* __restrict__ out_len, int accel,
-                                                   uint8_t* h_out, int32_t* h_done, uint8_t* blk, uint16_t* tab,
-                                                   lds_u8* ring, int32_t& solo_r) {
+                                                   uint8_t* h_out, int32_t* h_done, uint8_t* blk, uint8_t* obuf,
+                                                   uint16_t* tab, lds_u8* ring, int32_t& solo_r) {
     const uint32_t t = threadIdx.x;
     constexpr int kStep = 16 * 256;
     const int32_t lim = len + 64 < kSoloBuf ? len + 64 : kSoloBuf;   // the block and 64 zero bytes
+    uint32_t* ts = h_done ? reinterpret_cast<uint32_t*>(h_done + 1) : nullptr;   // CallMeta::work (LZ4M_WORKER_TS)
+    (void)ts;
+    LZ4M_WTS(ts, 0);
     for (int32_t base = 0; base < lim; base += kSoloU * kStep) {   // four pieces in flight per lane (16 measured no faster over PCIe)
         u32x4 v[kSoloU];
 #pragma unroll
@@ -720,32 +727,30 @@ __device__ __forceinline__ void compress_solo_body(const uint8_t* __restrict__ s
         }
     }
     __syncthreads();
+    LZ4M_WTS(ts, 1);
     if (t < kWave) {
-        const int64_t r = compress_block<V, ACC1>((const uint8_t*)blk, len, dst, cap, accel, tab, ring, t);
+        // a capacity at or above the bound parses as "not limited" whatever its
+        // size (lz4.c:1330-1343), so the bound is the LDS output's size
+        const int32_t bound = len + len / 255 + 16;
+        const int64_t r = compress_block<V, ACC1>((const uint8_t*)blk, len, obuf, cap < bound ? cap : bound, accel,
+                                                  tab, ring, t);
         if (t == 0) {
             *out_len = (int32_t)r;
             solo_r = (int32_t)r;
         }
     }
-    // the compressed bytes to the caller's mapped host buffer, all four waves,
-    // so the call needs no device-to-host copy of its own
     __syncthreads();
+    LZ4M_WTS(ts, 2);
+    // the compressed bytes from LDS to the caller's mapped host buffer (or to
+    // dst), all four waves: LDS reads and stores only, nothing waits on a store
     const int32_t r = solo_r;
-    for (int32_t base = 0; h_out != nullptr && base < r; base += kSoloU * kStep) {
-        u32x4 v[kSoloU];
-#pragma unroll
-        for (int u = 0; u < kSoloU; ++u) {
-            const int32_t p = base + u * kStep + 16 * (int32_t)t;
-            v[u] = p + 16 <= r ? ld16(dst + p) : ld16_guarded(dst + p, r - p);
-        }
-#pragma unroll
-        for (int u = 0; u < kSoloU; ++u) {
-            const int32_t p = base + u * kStep + 16 * (int32_t)t;
-            if (p + 16 <= r) {
-                st16(h_out + p, v[u]);
-            } else {
-                for (int32_t k = p; k < r; ++k) h_out[k] = dst[k];
-            }
+    uint8_t* out = h_out != nullptr ? h_out : dst;
+    for (int32_t p = 16 * (int32_t)t; p < r; p += kStep) {
+        const u32x4 v = lds_ld16((const lds_u8*)obuf + p);
+        if (p + 16 <= r) {
+            st16(out + p, v);
+        } else {
+            for (int32_t k = p; k < r; ++k) out[k] = obuf[k];
         }
     }
     if (h_done != nullptr) {   // all of the above visible to the host, then the flag it polls
@@ -754,6 +759,7 @@ __device__ __forceinline__ void compress_solo_body(const uint8_t* __restrict__ s
         // reach memory: ADVICE r03); then one thread stores the flag
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
         __syncthreads();
+        LZ4M_WTS(ts, 3);
         if (t == 0) __hip_atomic_store(h_done, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
@@ -947,6 +953,124 @@ __global__ __launch_bounds__(64) void compress_spec_kernel(
     }
 }
 
+// Late passes of the speculative linked compressor, when few blocks are left
+// to redo (pass j >= 1 redoes block b only if b-1's table changed in pass
+// j-1; on the synthetic mix 100 %, 26 %, 6 %, 1 % of the blocks in passes 1-4,
+// tools: CPU replay).  Such a pass is bound by ONE block's latency, and a
+// wave that reads its candidates and history from L2/HBM takes ~15 ms per
+// 64 KiB block.  Here one workgroup per redo block stages the block and its
+// 64 KiB of history in LDS (148 KiB with the table and ring: one workgroup
+// per CU), and wave 0 runs the same parse with every source read from LDS.
+//   compress_spec_list_kernel: blocks kept as they are hand their table on
+//     and the redo blocks are listed (counters[2]);
+//   compress_spec_lds_kernel: workgroup i redoes list[i] (grid = the number
+//     of tables the previous pass changed, which the host read).
+// Outputs, tables and change flags are exactly the batched pass's.
+constexpr int32_t kSpecLdsWin = 2 * (int32_t)kWin;   // history + a block of <= 64 KiB
+
+__global__ __launch_bounds__(256) void compress_spec_list_kernel(const int32_t* __restrict__ link, int64_t n,
+                                                                 const uint32_t* __restrict__ t_prev,
+                                                                 uint32_t* __restrict__ t_cur,
+                                                                 const uint8_t* __restrict__ chg_prev,
+                                                                 uint8_t* __restrict__ chg_cur, int32_t* counters,
+                                                                 int32_t* __restrict__ list) {
+    const uint32_t lane = threadIdx.x & 63;
+    for (int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); b < n; b += (int64_t)gridDim.x * 4) {
+        const bool linked = b > 0 && link[b] != 0;
+        if (linked && chg_prev[b - 1] != 0) {   // redo: listed for the LDS kernel
+            if (lane == 0) list[atomicAdd(&counters[2], 1)] = (int32_t)b;
+            continue;
+        }
+        const bool feeds = b + 1 < n && link[b + 1] != 0;
+        const u32x4* mine_prev = reinterpret_cast<const u32x4*>(t_prev + (size_t)b * 4096);
+        u32x4* mine_cur = reinterpret_cast<u32x4*>(t_cur + (size_t)b * 4096);
+        if (feeds)
+            for (int k = lane; k < 1024; k += kWave) mine_cur[k] = mine_prev[k];
+        if (lane == 0) chg_cur[b] = 0;
+    }
+}
+
+__global__ __launch_bounds__(256) void compress_spec_lds_kernel(
+    const uint8_t* __restrict__ src, const int64_t* __restrict__ src_off, const int32_t* __restrict__ src_len,
+    const int32_t* __restrict__ link, uint8_t* dst, const int64_t* __restrict__ dst_off,
+    const int32_t* __restrict__ dst_cap, int32_t* __restrict__ out_len, int64_t n, int accel,
+    const uint32_t* __restrict__ t_prev, uint32_t* __restrict__ t_cur, uint8_t* __restrict__ chg_cur,
+    int32_t* counters, const int32_t* __restrict__ list) {
+    __shared__ __attribute__((aligned(16))) uint8_t win[kSpecLdsWin + 64];
+    __shared__ __attribute__((aligned(16))) uint16_t tab[8192];
+    __shared__ int32_t diff_any;
+    RING_DECL
+    u32x4* t4 = reinterpret_cast<u32x4*>(tab);
+    const uint32_t t = threadIdx.x, lane = t & 63;
+    const int64_t b = list[blockIdx.x];   // linked, b >= 1, its predecessor's table changed
+    const bool feeds = b + 1 < n && link[b + 1] != 0;
+    const int32_t len = src_len[b];
+    if (src_len[b - 1] < (int32_t)kWin) {   // speculation needs >= 64 KiB predecessors (as compress_spec_kernel)
+        if (t == 0) {
+            atomicOr(&counters[1], 1);
+            out_len[b] = 0;
+            chg_cur[b] = 0;
+        }
+        return;
+    }
+    const int32_t hist = (int32_t)kWin;
+    const uint8_t* wg = src + src_off[b] - hist;
+    const bool staged = hist + len <= kSpecLdsWin;   // larger blocks parse from memory, as the batched pass
+    if (staged) {
+        constexpr int kU = 4, kStep = 16 * 256;
+        const int32_t lim = hist + len + 64;
+        for (int32_t base = 0; base < lim; base += kU * kStep) {
+            u32x4 v[kU];
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                const int32_t p = base + u * kStep + 16 * (int32_t)t;
+                v[u] = p + 16 <= hist + len ? ld16(wg + p) : ld16_guarded(wg + p, hist + len - p);
+            }
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                const int32_t p = base + u * kStep + 16 * (int32_t)t;
+                if (p < lim) lds_st16((lds_u8*)win + p, v[u]);
+            }
+        }
+    }
+    const u32x4* pred = reinterpret_cast<const u32x4*>(t_prev + (size_t)(b - 1) * 4096);
+    for (int k = t; k < 1024; k += 256) t4[k] = pred[k];
+    if (t == 0) diff_any = 0;
+    __syncthreads();
+    if (t < kWave) {
+        const uint8_t* w = staged ? (const uint8_t*)win : wg;
+        const int64_t r = compress_block_w<LZ4M_TABLE_U32_HASH5>(w, hist, len, dst + dst_off[b], dst_cap[b], accel, tab,
+                                                                 ring, lane, 0u, 0u, 0, 0);
+        if (lane == 0) out_len[b] = (int32_t)r;
+    }
+    __syncthreads();
+    if (!feeds) {
+        if (t == 0) chg_cur[b] = 0;
+        return;
+    }
+    // hand the table on in the successor's index space (as compress_spec_kernel)
+    const uint32_t shift = (uint32_t)(len + hist) - kWin;
+    const u32x4* mine_prev = reinterpret_cast<const u32x4*>(t_prev + (size_t)b * 4096);
+    u32x4* mine_cur = reinterpret_cast<u32x4*>(t_cur + (size_t)b * 4096);
+    bool diff = false;
+    for (int k = t; k < 1024; k += 256) {
+        u32x4 v = t4[k];
+        v.x = v.x > shift ? v.x - shift : 0u;
+        v.y = v.y > shift ? v.y - shift : 0u;
+        v.z = v.z > shift ? v.z - shift : 0u;
+        v.w = v.w > shift ? v.w - shift : 0u;
+        mine_cur[k] = v;
+        const u32x4 o = mine_prev[k];
+        diff |= (o.x != v.x) | (o.y != v.y) | (o.z != v.z) | (o.w != v.w);
+    }
+    if (__ballot(diff) != 0 && lane == 0) diff_any = 1;
+    __syncthreads();
+    if (t == 0) {
+        chg_cur[b] = diff_any ? 1 : 0;
+        if (diff_any) atomicAdd(&counters[0], 1);
+    }
+}
+
 
 // (the LDS buffers are the caller's: one set for the launch-per-call kernel,
 // one set shared by every table variant of the persistent worker)
@@ -956,9 +1080,10 @@ __global__ __launch_bounds__(256) void compress_solo_kernel(const uint8_t* __res
                                                             int accel, uint8_t* h_out, int32_t* h_done) {
     __shared__ int32_t solo_r;
     __shared__ __attribute__((aligned(16))) uint8_t blk[kSoloBuf];
+    __shared__ __attribute__((aligned(16))) uint8_t obuf[kSoloOut];
     __shared__ __attribute__((aligned(16))) uint16_t tab[8192];
     RING_DECL
-    compress_solo_body<V, ACC1>(src, len, dst, cap, out_len, accel, h_out, h_done, blk, tab, ring, solo_r);
+    compress_solo_body<V, ACC1>(src, len, dst, cap, out_len, accel, h_out, h_done, blk, obuf, tab, ring, solo_r);
 }
 
 // The single-call compress worker (lz4m_worker.h): one persistent workgroup
@@ -968,6 +1093,7 @@ __global__ __launch_bounds__(256) void compress_worker(Mailbox* mb, uint8_t* hd,
     __shared__ uint32_t cmd[8];
     __shared__ int32_t solo_r;
     __shared__ __attribute__((aligned(16))) uint8_t blk[kSoloBuf];
+    __shared__ __attribute__((aligned(16))) uint8_t obuf[kSoloOut];
     __shared__ __attribute__((aligned(16))) uint16_t tab[8192];
     RING_DECL
     uint32_t last = worker_init(mb, cmd);
@@ -983,17 +1109,17 @@ __global__ __launch_bounds__(256) void compress_worker(Mailbox* mb, uint8_t* hd,
         if (table == LZ4M_TABLE_U32_HASH5) {
             if (accel == 1)
                 compress_solo_body<LZ4M_TABLE_U32_HASH5, true>(hd, len, dbuf, cap, &rec->result, accel, hout, &rec->done,
-                                                              blk, tab, ring, solo_r);
+                                                              blk, obuf, tab, ring, solo_r);
             else
                 compress_solo_body<LZ4M_TABLE_U32_HASH5, false>(hd, len, dbuf, cap, &rec->result, accel, hout,
-                                                               &rec->done, blk, tab, ring, solo_r);
+                                                               &rec->done, blk, obuf, tab, ring, solo_r);
         } else {   // AUTO / U16: below 65547 bytes the byU16 parse (lz4.c:1352-1357)
             if (accel == 1)
                 compress_solo_body<LZ4M_TABLE_U16_HASH4, true>(hd, len, dbuf, cap, &rec->result, accel, hout, &rec->done,
-                                                              blk, tab, ring, solo_r);
+                                                              blk, obuf, tab, ring, solo_r);
             else
                 compress_solo_body<LZ4M_TABLE_U16_HASH4, false>(hd, len, dbuf, cap, &rec->result, accel, hout,
-                                                               &rec->done, blk, tab, ring, solo_r);
+                                                               &rec->done, blk, obuf, tab, ring, solo_r);
         }
     }
 }
@@ -1138,7 +1264,14 @@ extern "C" int lz4m_compress_linked_passes(void) { return g_linked_passes; }
 
 extern "C" size_t lz4m_compress_linked_workspace_size(int64_t n) {
     if (n <= 0) return 64;
-    return 64 + (size_t)n * 2 * 16384 + (((size_t)n * 2 + 63) & ~(size_t)63);
+    return 64 + (size_t)n * 2 * 16384 + (((size_t)n * 2 + 63) & ~(size_t)63) + (size_t)n * 4;
+}
+
+// LZ4M_SPEC_LDS: redo counts up to which a pass >= 1 runs the LDS-staged
+// kernels (default 2048; 0 = always the batched pass)
+static int64_t spec_lds_max() {
+    const char* e = getenv("LZ4M_SPEC_LDS");   // read per call (tests switch it)
+    return e ? (int64_t)atoll(e) : (int64_t)2048;
 }
 
 extern "C" int lz4m_compress_linked_batch(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len,
@@ -1161,23 +1294,39 @@ extern "C" int lz4m_compress_linked_batch(const uint8_t* d_src, const int64_t* d
     int32_t* counters = (int32_t*)base;
     uint32_t* tb[2] = {(uint32_t*)(base + 64), (uint32_t*)(base + 64 + (size_t)n * 16384)};
     uint8_t* cb[2] = {base + 64 + (size_t)n * 32768, base + 64 + (size_t)n * 32768 + (size_t)n};
-    int32_t h_counters[2] = {0, 0};
+    int32_t* list = (int32_t*)(base + 64 + (size_t)n * 32768 + (((size_t)n * 2 + 63) & ~(size_t)63));
+    int32_t h_counters[3] = {0, 0, 0};
     g_linked_passes = 0;
+    const int64_t lds_max = spec_lds_max();
     for (int64_t pass = 0; pass <= n; ++pass) {
         g_linked_passes = (int)pass + 1;
-        hipError_t e = hipMemsetAsync(counters, 0, 8, s);
+        hipError_t e = hipMemsetAsync(counters, 0, 12, s);
         if (e != hipSuccess) return (int)e;
         const int cur = (int)(pass & 1), prev = cur ^ 1;
-        hipLaunchKernelGGL(compress_spec_kernel, dim3(grid), dim3(64), 0, s, d_src, d_src_off, d_src_len, d_link,
-                           d_dst, d_dst_off, d_dst_cap, d_out_len, n, acceleration, tb[prev], tb[cur], cb[prev],
-                           cb[cur], counters, (int)pass);
+        const int64_t redo = h_counters[0];   // the previous pass's changed tables = this pass's redo blocks
+        if (pass > 0 && redo <= lds_max) {
+            const uint32_t lgrid = (uint32_t)((n + 3) / 4 < 65536 ? (n + 3) / 4 : 65536);
+            hipLaunchKernelGGL(compress_spec_list_kernel, dim3(lgrid), dim3(256), 0, s, d_link, n, tb[prev], tb[cur],
+                               cb[prev], cb[cur], counters, list);
+            if (redo > 0)
+                hipLaunchKernelGGL(compress_spec_lds_kernel, dim3((uint32_t)redo), dim3(256), 0, s, d_src, d_src_off,
+                                   d_src_len, d_link, d_dst, d_dst_off, d_dst_cap, d_out_len, n, acceleration,
+                                   tb[prev], tb[cur], cb[cur], counters, list);
+        } else {
+            hipLaunchKernelGGL(compress_spec_kernel, dim3(grid), dim3(64), 0, s, d_src, d_src_off, d_src_len, d_link,
+                               d_dst, d_dst_off, d_dst_cap, d_out_len, n, acceleration, tb[prev], tb[cur], cb[prev],
+                               cb[cur], counters, (int)pass);
+        }
         e = hipGetLastError();
         if (e != hipSuccess) return (int)e;
-        e = hipMemcpyAsync(h_counters, counters, 8, hipMemcpyDeviceToHost, s);
+        e = hipMemcpyAsync(h_counters, counters, 12, hipMemcpyDeviceToHost, s);
         if (e == hipSuccess) e = hipStreamSynchronize(s);
         if (e != hipSuccess) return (int)e;
         if (h_counters[1]) return LZ4M_EINVAL;
-        if (getenv("LZ4M_SPEC_VERBOSE")) fprintf(stderr, "[lz4m] linked pass %d: %d tables changed\n", (int)pass, h_counters[0]);
+        if (getenv("LZ4M_SPEC_VERBOSE"))
+            fprintf(stderr, "[lz4m] linked pass %d: %lld redone%s, %d tables changed\n", (int)pass,
+                    (long long)(pass == 0 ? n : redo), pass > 0 && redo <= lds_max ? " (LDS-staged)" : "",
+                    h_counters[0]);
         if (h_counters[0] == 0) return 0;
     }
     return 0;

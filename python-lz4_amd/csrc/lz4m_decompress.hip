@@ -147,7 +147,10 @@ __device__ __forceinline__ void lane_match(uint8_t* d, int64_t off, int64_t len,
 // Literal bytes never overlap their destination, so each lane requests four
 // 16-byte pieces before storing any: a long literal (a stored-looking block's
 // 64 KiB) waits on one memory round trip per 4 KiB instead of per 1 KiB.
-template <int kU = 4>   // pieces per lane per round trip (1 where registers are short: the dictionary kernel)
+// SL: s points into LDS (the lone-block decoder's staged input): LDS reads,
+// which wait on no store, where a flat read of LDS waits for every store the
+// wave has in flight (one L2 write round trip per 4 KiB of a long literal).
+template <int kU = 4, bool SL = false>   // kU: pieces per lane per round trip (1 where registers are short: the dictionary kernel)
 __device__ __forceinline__ void wave_literal(uint8_t* d, const uint8_t* s, int64_t len, int64_t d_room,
                                              int64_t s_room, uint32_t lane) {
     for (int64_t base = 0; base < len; base += 16 * kWave * kU) {
@@ -156,7 +159,10 @@ __device__ __forceinline__ void wave_literal(uint8_t* d, const uint8_t* s, int64
         for (int u = 0; u < kU; ++u) {
             const int64_t pos = base + 16 * kWave * u + 16 * (int64_t)lane;
             const bool whole = pos < len && (len - pos >= 16 || s_room - pos >= 16);
-            v[u] = whole ? ld16(s + pos) : u32x4{0, 0, 0, 0};
+            if constexpr (SL)
+                v[u] = whole ? lds_ld16a((const lds_u8*)(s + pos)) : u32x4{0, 0, 0, 0};
+            else
+                v[u] = whole ? ld16(s + pos) : u32x4{0, 0, 0, 0};
         }
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
@@ -565,6 +571,7 @@ __device__ __forceinline__ int32_t coop_incl_sum(int32_t v) {
 
 // Exact-length whole-wave copies (no wild bytes: other sequences' output may
 // already sit right after them).
+template <bool SL = false>   // SL: s points into LDS (as wave_literal)
 __device__ __forceinline__ void coop_copy_literal(uint8_t* d, const uint8_t* s, int32_t len, uint32_t lane) {
     constexpr int kU = 4;   // four pieces requested before any is stored (as wave_literal)
     for (int32_t base = 0; base < len; base += 16 * kWave * kU) {
@@ -572,7 +579,10 @@ __device__ __forceinline__ void coop_copy_literal(uint8_t* d, const uint8_t* s, 
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
             const int32_t pos = base + 16 * kWave * u + 16 * (int32_t)lane;
-            v[u] = pos < len ? ld16(s + pos) : u32x4{0, 0, 0, 0};
+            if constexpr (SL)
+                v[u] = pos < len ? lds_ld16a((const lds_u8*)(s + pos)) : u32x4{0, 0, 0, 0};
+            else
+                v[u] = pos < len ? ld16(s + pos) : u32x4{0, 0, 0, 0};
         }
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
@@ -656,8 +666,9 @@ __device__ __forceinline__ CoopSeq coop_parse(const lds_u8* IN, int32_t t, u32x4
 // reference's result (decoded size or -(error position)-1).  Output [0, op)
 // must already be in HBM and visible to the wave.
 // DICT: the dlen bytes before dict_end are the block's dictionary
-// (LZ4_decompress_safe_usingDict, as decompress_kernel<true>).
-template <bool DICT = false>
+// (LZ4_decompress_safe_usingDict, as decompress_kernel<true>).  SL: s points
+// into LDS (long literals read as LDS, wave_literal).
+template <bool DICT = false, bool SL = false>
 __device__ __forceinline__ int32_t coop_finish(const uint8_t* s, uint8_t* d, int32_t iend, int32_t oend, int32_t ip,
                                                int32_t op, bool fast, uint32_t lane, int32_t dlen = 0,
                                                const uint8_t* dict_end = nullptr) {
@@ -685,7 +696,7 @@ __device__ __forceinline__ int32_t coop_finish(const uint8_t* s, uint8_t* d, int
         if (__builtin_amdgcn_readlane(lc.kind, 0) != kNone) {
             const int64_t ie = readlane64(L.iend, 0);
             const int64_t dp = readlane64(lc.dpos, 0), sp = readlane64(lc.arg, 0), ln = readlane64(lc.len, 0);
-            wave_literal<DICT ? 1 : 4>(d + dp, s + sp, ln, oe - dp, ie - sp, lane);   // DICT: registers are short
+            wave_literal<DICT ? 1 : 4, SL>(d + dp, s + sp, ln, oe - dp, ie - sp, lane);   // DICT: registers are short
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
         }
         if (__builtin_amdgcn_readlane(mc.kind, 0) != kNone) {
@@ -848,7 +859,10 @@ __device__ __forceinline__ void hist_decompress_body(const uint8_t* __restrict__
     HP_DECL
     const uint8_t* solo_src = nullptr;
     __shared__ int32_t solo_r;
+    uint32_t* ts = SOLO && solo_done ? reinterpret_cast<uint32_t*>(solo_done + 1) : nullptr;   // CallMeta::work
+    (void)ts;
     if constexpr (SOLO) {
+        LZ4M_WTS(ts, 0);
         __shared__ __attribute__((aligned(16))) uint8_t sblk[kSoloIn];
         const uint8_t* g = src + src_off[0];
         const int32_t len = src_len[0];   // <= kSoloIn - 64 (host-checked); zeros past it
@@ -868,6 +882,7 @@ __device__ __forceinline__ void hist_decompress_body(const uint8_t* __restrict__
             }
         }
         __syncthreads();
+        LZ4M_WTS(ts, 1);
         solo_src = (const uint8_t*)sblk;
     }
     for (int64_t b = (int64_t)blockIdx.x * 4 + wv; b < n; b += (int64_t)gridDim.x * 4) {
@@ -978,7 +993,7 @@ __device__ __forceinline__ void hist_decompress_body(const uint8_t* __restrict__
                 for (int32_t c = F + 16 * (int32_t)lane; c < op; c += 16 * kWave)
                     coop_put(d + c, lds_ld16(OB + (c - base)), op - c);
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-                coop_copy_literal(d + op, s + q, lit, lane);
+                coop_copy_literal<SOLO>(d + op, s + q, lit, lane);
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
                 coop_copy_match(d + opm, off, ml, lane);
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
@@ -1089,7 +1104,7 @@ __device__ __forceinline__ void hist_decompress_body(const uint8_t* __restrict__
         for (int32_t c = F + 16 * (int32_t)lane; c < op; c += 16 * kWave)
             coop_put(d + c, lds_ld16(OB + (c - base)), op - c);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-        const int32_t r = coop_finish<DICT>(s, d, iend, oend, ip, op, fast, lane, dlen, d + ddelta);
+        const int32_t r = coop_finish<DICT, SOLO>(s, d, iend, oend, ip, op, fast, lane, dlen, d + ddelta);
         if (lane == 0) status[b] = r;
         if (SOLO && lane == 0) solo_r = r;
         HP_MARK(7);
@@ -1100,26 +1115,41 @@ __device__ __forceinline__ void hist_decompress_body(const uint8_t* __restrict__
         // (wave 0 decoded; the others skipped the loop), so the call needs no
         // device-to-host copy of its own
         __syncthreads();
+        LZ4M_WTS(ts, 2);
         const int32_t r = solo_r;
         if (solo_out != nullptr && r > 0) {
+            // through LDS (the staged input is no longer needed): every wave
+            // first loads a chunk of the output into LDS, then stores it from
+            // LDS, so no load waits behind the stores to host memory in flight
+            // (a wave's memory counter retires in order)
             const uint8_t* d0 = dst + dst_off[0];
-            constexpr int32_t kStep = 16 * 256;
-            for (int32_t base0 = 0; base0 < r; base0 += kSoloU * kStep) {
-                u32x4 v[kSoloU];
+            constexpr int32_t kStep = 16 * 256, kChunk = 16 * kStep;   // 64 KiB <= kSoloIn
+            lds_u8* bounce = (lds_u8*)const_cast<uint8_t*>(solo_src);   // the staging buffer (kSoloIn)
+            for (int32_t c0 = 0; c0 < r; c0 += kChunk) {
+                const int32_t m = r - c0 < kChunk ? r - c0 : kChunk;
+                for (int32_t base0 = 0; base0 < m; base0 += kSoloU * kStep) {
+                    u32x4 v[kSoloU];
 #pragma unroll
-                for (int u = 0; u < kSoloU; ++u) {
-                    const int32_t p = base0 + u * kStep + 16 * (int32_t)threadIdx.x;
-                    v[u] = p + 16 <= r ? ld16(d0 + p) : ld16_guarded(d0 + p, r - p);
-                }
+                    for (int u = 0; u < kSoloU; ++u) {
+                        const int32_t p = base0 + u * kStep + 16 * (int32_t)threadIdx.x;
+                        v[u] = p + 16 <= m ? ld16(d0 + c0 + p) : ld16_guarded(d0 + c0 + p, m - p);
+                    }
 #pragma unroll
-                for (int u = 0; u < kSoloU; ++u) {
-                    const int32_t p = base0 + u * kStep + 16 * (int32_t)threadIdx.x;
-                    if (p + 16 <= r) {
-                        st16(solo_out + p, v[u]);
-                    } else if (p < r) {
-                        put_exact(solo_out + p, v[u], (uint32_t)(r - p));
+                    for (int u = 0; u < kSoloU; ++u) {
+                        const int32_t p = base0 + u * kStep + 16 * (int32_t)threadIdx.x;
+                        if (p < m) lds_st16(bounce + p, v[u]);
                     }
                 }
+                __syncthreads();
+                for (int32_t p = 16 * (int32_t)threadIdx.x; p < m; p += kStep) {
+                    const u32x4 v = lds_ld16(bounce + p);
+                    if (p + 16 <= m) {
+                        st16(solo_out + c0 + p, v);
+                    } else {
+                        put_exact(solo_out + c0 + p, v, (uint32_t)(m - p));
+                    }
+                }
+                __syncthreads();
             }
         }
         if (solo_done != nullptr) {   // all of the above visible to the host, then the flag it polls
@@ -1127,6 +1157,7 @@ __device__ __forceinline__ void hist_decompress_body(const uint8_t* __restrict__
             // scope before the barrier, then one thread stores the flag
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
             __syncthreads();
+            LZ4M_WTS(ts, 3);
             if (threadIdx.x == 0) __hip_atomic_store(solo_done, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }

@@ -403,7 +403,8 @@ extern "C" int lz4m_compress_block_api_staged(const char* src, int srcSize, int 
 // diagnostics (tests, probes): out[0..7] = this thread's decompress / compress
 // mailbox seq, served, quit, and the launched flags; out[8..11] = per kind the
 // requests its last launch served and how that launch ended (1 idle, 2 quit);
-// returns the failure count
+// out[12..15] = per kind the poll's two real-time stamps (LZ4M_WORKER_TS
+// builds); returns the failure count
 extern "C" int lz4m_single_call_worker_state(uint32_t* out) {
     Workers& W = t_workers;
     for (int k = 0; k < 2; ++k) {
@@ -413,6 +414,8 @@ extern "C" int lz4m_single_call_worker_state(uint32_t* out) {
         out[3 * k + 2] = M ? __atomic_load_n(&M->quit, __ATOMIC_ACQUIRE) : 0u;
         out[8 + 2 * k] = M ? __atomic_load_n(&M->pad[0], __ATOMIC_ACQUIRE) : 0u;
         out[9 + 2 * k] = M ? __atomic_load_n(&M->pad[1], __ATOMIC_ACQUIRE) : 0u;
+        out[12 + 2 * k] = M ? __atomic_load_n(&M->pad[2], __ATOMIC_ACQUIRE) : 0u;   // LZ4M_WORKER_TS builds
+        out[13 + 2 * k] = M ? __atomic_load_n(&M->pad[3], __ATOMIC_ACQUIRE) : 0u;
     }
     out[6] = W.launched[0];
     out[7] = W.launched[1];

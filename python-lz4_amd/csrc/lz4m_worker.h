@@ -38,6 +38,22 @@ struct Mailbox {
 };
 static_assert(sizeof(Mailbox) == 64 && offsetof(Mailbox, rec_off) == 16, "mailbox layout");
 
+// LZ4M_WORKER_TS (diagnostic builds only): lane 0 stamps the 100 MHz real-time
+// clock at each stage of a lone-block call into the record's work[] words
+// (bodies) and the mailbox's pad[2..3] (poll), for tools/probe_wts.py.
+#ifdef LZ4M_WORKER_TS
+#define LZ4M_WTS(ptr, i)                                                                                  \
+    do {                                                                                                  \
+        if (threadIdx.x == 0 && (ptr) != nullptr)                                                         \
+            __hip_atomic_store((uint32_t*)(ptr) + (i), (uint32_t)__builtin_amdgcn_s_memrealtime(),         \
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);                              \
+    } while (0)
+#else
+#define LZ4M_WTS(ptr, i) \
+    do {                 \
+    } while (0)
+#endif
+
 // the request a worker serves next, broadcast to the workgroup (lane 0 polls);
 // 0 = exit.  Fields of the request land in cmd[1..5]; cmd[6] counts the
 // requests served.  `last` is the request just served (0: none yet): once every
@@ -58,7 +74,10 @@ __device__ __forceinline__ uint32_t worker_next(Mailbox* mb, uint32_t& last, uin
                 why = 2;
                 break;
             }
-            if (seq != last) break;
+            if (seq != last) {
+                LZ4M_WTS(&mb->pad[2], 0);
+                break;
+            }
             if (__builtin_amdgcn_s_memrealtime() - t0 > idle) {
                 why = 1;
                 break;
@@ -80,6 +99,7 @@ __device__ __forceinline__ uint32_t worker_next(Mailbox* mb, uint32_t& last, uin
         cmd[3] = f.z;
         cmd[4] = f.w;
         cmd[5] = acc;
+        LZ4M_WTS(&mb->pad[3], 0);
     }
     __syncthreads();
     last = cmd[0];

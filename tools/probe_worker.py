@@ -11,7 +11,7 @@ sys.path.insert(0, os.path.join(ROOT, "python-lz4_amd"))
 import lz4._native as N  # noqa: E402
 
 lib = N.lib()
-st = (C.c_uint32 * 12)()
+st = (C.c_uint32 * 16)()
 
 
 def show(tag):
