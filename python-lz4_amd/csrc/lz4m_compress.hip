@@ -24,6 +24,7 @@
 #include "lz4m_common.h"
 #include "lz4m_worker.h"
 
+#include <chrono>
 #include <type_traits>
 
 #include <stdio.h>
@@ -955,12 +956,13 @@ __global__ __launch_bounds__(64) void compress_spec_kernel(
 
 // Late passes of the speculative linked compressor, when few blocks are left
 // to redo (pass j >= 1 redoes block b only if b-1's table changed in pass
-// j-1; on the synthetic mix 100 %, 26 %, 6 %, 1 % of the blocks in passes 1-4,
-// tools: CPU replay).  Such a pass is bound by ONE block's latency, and a
-// wave that reads its candidates and history from L2/HBM takes ~15 ms per
-// 64 KiB block.  Here one workgroup per redo block stages the block and its
-// 64 KiB of history in LDS (148 KiB with the table and ring: one workgroup
-// per CU), and wave 0 runs the same parse with every source read from LDS.
+// j-1; on 4 096 silesia-like blocks 4 095, 1 051, 216, 14 in passes 1-4).
+// Such a pass is bound by ONE block's latency: 16.3 ms for a wave that reads
+// its candidates and history from L2/HBM.  Here one workgroup per redo block
+// stages the block and its 64 KiB of history in LDS (148 KiB with the table
+// and ring: one workgroup per CU), and wave 0 runs the same parse with every
+// source read from LDS: 13.6 ms.  The serial parse itself (~5 000 cycles per
+// sequence, ~6 300 sequences) is what remains.
 //   compress_spec_list_kernel: blocks kept as they are hand their table on
 //     and the redo blocks are listed (counters[2]);
 //   compress_spec_lds_kernel: workgroup i redoes list[i] (grid = the number
@@ -1038,9 +1040,16 @@ __global__ __launch_bounds__(256) void compress_spec_lds_kernel(
     if (t == 0) diff_any = 0;
     __syncthreads();
     if (t < kWave) {
-        const uint8_t* w = staged ? (const uint8_t*)win : wg;
-        const int64_t r = compress_block_w<LZ4M_TABLE_U32_HASH5>(w, hist, len, dst + dst_off[b], dst_cap[b], accel, tab,
-                                                                 ring, lane, 0u, 0u, 0, 0);
+        // two call sites, so that the staged one compiles to LDS instructions
+        // (a pointer that may be either is a flat one: every flat load also
+        // waits for the wave's stores in flight)
+        int64_t r;
+        if (staged)
+            r = compress_block_w<LZ4M_TABLE_U32_HASH5>((const uint8_t*)win, hist, len, dst + dst_off[b], dst_cap[b],
+                                                       accel, tab, ring, lane, 0u, 0u, 0, 0);
+        else
+            r = compress_block_w<LZ4M_TABLE_U32_HASH5>(wg, hist, len, dst + dst_off[b], dst_cap[b], accel, tab, ring,
+                                                       lane, 0u, 0u, 0, 0);
         if (lane == 0) out_len[b] = (int32_t)r;
     }
     __syncthreads();
@@ -1268,10 +1277,13 @@ extern "C" size_t lz4m_compress_linked_workspace_size(int64_t n) {
 }
 
 // LZ4M_SPEC_LDS: redo counts up to which a pass >= 1 runs the LDS-staged
-// kernels (default 2048; 0 = always the batched pass)
+// kernels (0 = always the batched pass).  Default 256, one workgroup per CU:
+// a lone 64 KiB silesia-like block takes 13.6 ms staged against 16.3 ms in
+// the batched kernel, but a pass of 1 051 staged blocks (5 rounds of 256 CUs)
+// took 46 ms against 20.5 (profiles/r04/r04r_time_linked_*.log)
 static int64_t spec_lds_max() {
     const char* e = getenv("LZ4M_SPEC_LDS");   // read per call (tests switch it)
-    return e ? (int64_t)atoll(e) : (int64_t)2048;
+    return e ? (int64_t)atoll(e) : (int64_t)256;
 }
 
 extern "C" int lz4m_compress_linked_batch(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len,
@@ -1298,6 +1310,8 @@ extern "C" int lz4m_compress_linked_batch(const uint8_t* d_src, const int64_t* d
     int32_t h_counters[3] = {0, 0, 0};
     g_linked_passes = 0;
     const int64_t lds_max = spec_lds_max();
+    const bool verbose = getenv("LZ4M_SPEC_VERBOSE") != nullptr;
+    auto t_prev = std::chrono::steady_clock::now();
     for (int64_t pass = 0; pass <= n; ++pass) {
         g_linked_passes = (int)pass + 1;
         hipError_t e = hipMemsetAsync(counters, 0, 12, s);
@@ -1323,10 +1337,13 @@ extern "C" int lz4m_compress_linked_batch(const uint8_t* d_src, const int64_t* d
         if (e == hipSuccess) e = hipStreamSynchronize(s);
         if (e != hipSuccess) return (int)e;
         if (h_counters[1]) return LZ4M_EINVAL;
-        if (getenv("LZ4M_SPEC_VERBOSE"))
-            fprintf(stderr, "[lz4m] linked pass %d: %lld redone%s, %d tables changed\n", (int)pass,
+        if (verbose) {   // (the host waits for every pass: its wall time is the pass's)
+            const auto t_now = std::chrono::steady_clock::now();
+            fprintf(stderr, "[lz4m] linked pass %d: %lld redone%s, %d tables changed, %.2f ms\n", (int)pass,
                     (long long)(pass == 0 ? n : redo), pass > 0 && redo <= lds_max ? " (LDS-staged)" : "",
-                    h_counters[0]);
+                    h_counters[0], std::chrono::duration<double, std::milli>(t_now - t_prev).count());
+            t_prev = t_now;
+        }
         if (h_counters[0] == 0) return 0;
     }
     return 0;

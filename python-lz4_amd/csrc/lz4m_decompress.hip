@@ -1101,10 +1101,13 @@ __device__ __forceinline__ void hist_decompress_body(const uint8_t* __restrict__
             if (use < nseq && !fit_only) break;
         }
         // flush the rest exactly, then the exact state machine from (ip, op)
+        if (SOLO) LZ4M_WTS(ts, 4);
         for (int32_t c = F + 16 * (int32_t)lane; c < op; c += 16 * kWave)
             coop_put(d + c, lds_ld16(OB + (c - base)), op - c);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        if (SOLO) LZ4M_WTS(ts, 5);
         const int32_t r = coop_finish<DICT, SOLO>(s, d, iend, oend, ip, op, fast, lane, dlen, d + ddelta);
+        if (SOLO) LZ4M_WTS(ts, 6);
         if (lane == 0) status[b] = r;
         if (SOLO && lane == 0) solo_r = r;
         HP_MARK(7);

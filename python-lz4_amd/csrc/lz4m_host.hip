@@ -182,16 +182,19 @@ bool worker_enabled() {
 
 struct Workers {
     int dev = -1;
-    uint8_t* host = nullptr;       // [mailbox 0 | mailbox 1] then per kind [input kWorkIn] [record kMeta] [output kWorkOut]
+    uint8_t* host = nullptr;       // [mailbox 0 | mailbox 1] (coherent)
     uint8_t* host_dev = nullptr;
+    uint8_t* data = nullptr;       // per kind [input kWorkIn] [record kMeta] [output kWorkOut]
+    uint8_t* data_dev = nullptr;
+    bool data_own = false;         // data is its own allocation (LZ4M_WORKER_MEM=nc)
     uint8_t* dbuf = nullptr;       // device output buffers, one per kind
     hipStream_t stream[2] = {nullptr, nullptr};
     bool launched[2] = {false, false};
     uint32_t seq[2] = {0, 0};
     lz4m::Mailbox* mb(int k) { return reinterpret_cast<lz4m::Mailbox*>(host + 64 * k); }
     static constexpr size_t kRegion = kWorkIn + kMeta + kWorkOut + 256;
-    size_t region(int k) const { return kWorkMb + (size_t)k * kRegion; }
-    uint8_t* base(int k) { return host + region(k); }
+    size_t region(int k) const { return (size_t)k * kRegion; }
+    uint8_t* base(int k) { return data + region(k); }
     bool idle(int k) { return hipStreamQuery(stream[k]) == hipSuccess; }
     void stop(int k) {
         if (!launched[k]) return;
@@ -209,7 +212,9 @@ struct Workers {
             if (stream[k]) (void)hipStreamDestroy(stream[k]);
         if (dbuf) (void)hipFree(dbuf);
         if (host) (void)hipHostFree(host);
-        host = host_dev = dbuf = nullptr;
+        if (data && data_own) (void)hipHostFree(data);
+        data_own = false;
+        host = host_dev = dbuf = data = data_dev = nullptr;
         stream[0] = stream[1] = nullptr;
     }
     ~Workers() { release(); }
@@ -221,14 +226,29 @@ struct Workers {
             dev = d;
         }
         if (host) return true;
-        const size_t bytes = kWorkMb + 2 * kRegion;
-        // coherent (fine-grained): the worker reads the mailbox and each request's bytes
-        // while it runs, with no kernel boundary to invalidate a cached copy
-        if (hipHostMalloc(reinterpret_cast<void**>(&host), bytes, hipHostMallocMapped | hipHostMallocCoherent) !=
-            hipSuccess)
+        // the mailboxes are coherent (fine-grained): the worker polls them
+        // while it runs, with no kernel boundary to invalidate a cached copy.
+        // The request bytes: coherent too by default; LZ4M_WORKER_MEM=nc maps
+        // them non-coherent (cached in L2: the worker's system-scope acquire
+        // after each poll invalidates, its release writes back)
+        const char* me = getenv("LZ4M_WORKER_MEM");
+        const bool nc = me != nullptr && strcmp(me, "nc") == 0;
+        const unsigned cflags = hipHostMallocMapped | hipHostMallocCoherent;
+        if (hipHostMalloc(reinterpret_cast<void**>(&host), nc ? kWorkMb : kWorkMb + 2 * kRegion, cflags) != hipSuccess)
             return false;
         memset(host, 0, kWorkMb);
+        if (nc) {
+            if (hipHostMalloc(reinterpret_cast<void**>(&data), 2 * kRegion, hipHostMallocMapped | hipHostMallocNonCoherent) !=
+                hipSuccess) {
+                release();
+                return false;
+            }
+            data_own = true;
+        } else {
+            data = host + kWorkMb;
+        }
         if (hipHostGetDevicePointer(reinterpret_cast<void**>(&host_dev), host, 0) != hipSuccess ||
+            hipHostGetDevicePointer(reinterpret_cast<void**>(&data_dev), data, 0) != hipSuccess ||
             hipMalloc(reinterpret_cast<void**>(&dbuf), 2 * (kWorkOut + 256)) != hipSuccess) {
             release();
             return false;
@@ -244,7 +264,7 @@ struct Workers {
         if (launched[k] && idle(k)) launched[k] = false;   // exited (idle or quit)
         if (launched[k]) return true;
         __atomic_store_n(&mb(k)->quit, 0u, __ATOMIC_RELEASE);
-        if (lz4m_worker_launch(k, reinterpret_cast<lz4m::Mailbox*>(host_dev + 64 * k), host_dev + region(k),
+        if (lz4m_worker_launch(k, reinterpret_cast<lz4m::Mailbox*>(host_dev + 64 * k), data_dev + region(k),
                                dbuf + (size_t)k * (kWorkOut + 256), kIdle, stream[k]) != 0)
             return false;
         launched[k] = true;

@@ -287,11 +287,11 @@ def test_linked_blocks_vs_oracle(gpu, oracle, mode, monkeypatch):
     orc_compress_linked (pinned to the reference's linked frames).
     "speculative" runs every pass >= 1 of these small streams with the
     LDS-staged kernels (compress_spec_lds_kernel; blocks > 64 KiB parse from
-    memory there), "speculative-batched" with the batched pass
-    (LZ4M_SPEC_LDS=0)."""
+    memory there; threshold raised so every late pass takes them),
+    "speculative-batched" with the batched pass (LZ4M_SPEC_LDS=0)."""
     import lz4._native as N
     from lz4 import _synth
-    monkeypatch.setenv("LZ4M_SPEC_LDS", "0" if mode == "speculative-batched" else "2048")
+    monkeypatch.setenv("LZ4M_SPEC_LDS", "0" if mode == "speculative-batched" else "100000")
     m = N.LINKED_SERIAL if mode == "serial" else N.LINKED_SPECULATIVE
     for kind in ("silesia", "text", "records", "runs", "random", "markup"):
         blob = _synth.blocks(48, kind, seed=5).tobytes()

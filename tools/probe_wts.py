@@ -42,6 +42,7 @@ for name, kind, f in cases:
     for _ in range(20):
         f()
     acc = [0.0] * 5
+    sub = [0.0] * 3
     wall = 0.0
     reps = 300
     for _ in range(reps):
@@ -49,11 +50,17 @@ for name, kind, f in cases:
         f()
         wall += time.perf_counter() - t
         lib.lz4m_single_call_worker_state(st)
-        w = (C.c_uint32 * 4).from_address(p.value - 256 + 32)
+        w = (C.c_uint32 * 8).from_address(p.value - 256 + 32)
         seen, fields = st[12 + 2 * kind], st[13 + 2 * kind]
         marks = [seen, fields, w[0], w[1], w[2], w[3]]
         for i in range(5):
             acc[i] += ((marks[i + 1] - marks[i]) & 0xFFFFFFFF) / 100.0   # 100 MHz ticks -> us
+        if kind == 0 and w[5] and w[6]:   # decoder: rounds / flush / exact tail inside "compute"
+            sub[0] += ((w[4] - w[1]) & 0xFFFFFFFF) / 100.0
+            sub[1] += ((w[5] - w[4]) & 0xFFFFFFFF) / 100.0
+            sub[2] += ((w[6] - w[5]) & 0xFFFFFFFF) / 100.0
     dev = sum(acc) / reps
     print(f"{name}: wall {wall / reps * 1e6:.1f} us, device poll->done {dev:.1f} us: " +
-          ", ".join(f"{n} {a / reps:.2f}" for n, a in zip(names, acc)), flush=True)
+          ", ".join(f"{n} {a / reps:.2f}" for n, a in zip(names, acc)) +
+          (f" [rounds {sub[0] / reps:.2f}, flush {sub[1] / reps:.2f}, exact tail {sub[2] / reps:.2f}]" if sub[2] else ""),
+          flush=True)

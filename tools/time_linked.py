@@ -1,6 +1,6 @@
 """Time linked-block compression (serial vs speculative) on device data.
 usage: python tools/time_linked.py [MiB] [kinds...]"""
-import sys, time
+import os, sys, time
 sys.path.insert(0, "python-lz4_amd")
 import torch
 import lz4._native as N
@@ -14,7 +14,7 @@ for kind in kinds:
     data = _synth.blocks(mib * 16, kind, seed=3)
     d = torch.from_numpy(data.reshape(-1)).to(dev)
     n = d.numel()
-    for bsize in (65536, 4 << 20):
+    for bsize in [int(x) for x in os.environ.get("BSIZES", "65536,4194304").split(",")]:
         nb = (n + bsize - 1) // bsize
         off = torch.arange(nb, dtype=torch.int64, device=dev) * bsize
         ln = torch.full((nb,), bsize, dtype=torch.int32, device=dev)
