@@ -858,7 +858,7 @@ __device__ __forceinline__ void hist_decompress_body(const uint8_t* __restrict__
 #endif
     HP_DECL
     const uint8_t* solo_src = nullptr;
-    __shared__ int32_t solo_r;
+    __shared__ int32_t solo_r, solo_lit, solo_lip;   // SOLO: result; the stored-like fast path's length and start
     uint32_t* ts = SOLO && solo_done ? reinterpret_cast<uint32_t*>(solo_done + 1) : nullptr;   // CallMeta::work
     (void)ts;
     if constexpr (SOLO) {
@@ -884,8 +884,58 @@ __device__ __forceinline__ void hist_decompress_body(const uint8_t* __restrict__
         __syncthreads();
         LZ4M_WTS(ts, 1);
         solo_src = (const uint8_t*)sblk;
+        // A stored-like block -- one literal run to the end of the input, what
+        // LZ4 makes of incompressible data -- is one length read and one copy
+        // in the reference too (lz4.c:2000-2010 read_variable_length, then the
+        // last-literals branch :2205-2229 with ip + length == iend, op +
+        // length <= oend).  With the token's literal nibble 15, length L >= 15
+        // and the run ending exactly at iend, every check the reference makes
+        // on the way passes (the length bytes end at iend - L <= iend - 15, the
+        // read limit) and the result is L; anything else takes the decoder.
+        // Wave 0 finds the length run 64 bytes per ballot; every thread then
+        // copies the literal from LDS to the output and the caller's buffer.
+        if (threadIdx.x < kWave) {
+            const int32_t iend = src_len[0], oend = dst_cap[0];
+            int32_t q = -1, L = 15;
+            if (iend >= 17 && oend >= 15 && (sblk[0] >> 4) == 15) {
+                for (int32_t base = 1; base < iend; base += kWave) {
+                    const int32_t p = base + (int32_t)lane;
+                    const uint32_t bt = p < iend ? (uint32_t)sblk[p] : 0u;
+                    const uint64_t stop = __ballot(bt != 255u);
+                    if (stop == 0) {
+                        L += 255 * kWave;
+                        continue;
+                    }
+                    const int f = __builtin_ctzll(stop);
+                    L += 255 * f + __builtin_amdgcn_readlane((int)bt, f);
+                    q = base + f + 1;
+                    break;
+                }
+            }
+            if (lane == 0) solo_lit = (q > 0 && q + L == iend && L <= oend) ? L : -1, solo_lip = q;
+        }
+        __syncthreads();
+        if (solo_lit >= 0) {
+            const int32_t L = solo_lit;
+            const lds_u8* lit = (const lds_u8*)sblk + solo_lip;
+            uint8_t* d0 = dst + dst_off[0];
+            for (int32_t p = 16 * (int32_t)threadIdx.x; p < L; p += 16 * 256) {
+                const u32x4 v = lds_ld16a(lit + p);
+                if (p + 16 <= L) {
+                    st16(d0 + p, v);
+                    if (solo_out != nullptr) st16(solo_out + p, v);
+                } else {
+                    put_exact(d0 + p, v, (uint32_t)(L - p));
+                    if (solo_out != nullptr) put_exact(solo_out + p, v, (uint32_t)(L - p));
+                }
+            }
+            if (threadIdx.x == 0) {
+                status[0] = L;
+                solo_r = L;
+            }
+        }
     }
-    for (int64_t b = (int64_t)blockIdx.x * 4 + wv; b < n; b += (int64_t)gridDim.x * 4) {
+    for (int64_t b = (int64_t)blockIdx.x * 4 + wv; b < n && !(SOLO && solo_lit >= 0); b += (int64_t)gridDim.x * 4) {
         const uint8_t* s = SOLO ? solo_src : src + src_off[b];
         uint8_t* d = dst + dst_off[b];
         const int32_t iend = src_len[b], oend = dst_cap[b];
@@ -1120,7 +1170,7 @@ __device__ __forceinline__ void hist_decompress_body(const uint8_t* __restrict__
         __syncthreads();
         LZ4M_WTS(ts, 2);
         const int32_t r = solo_r;
-        if (solo_out != nullptr && r > 0) {
+        if (solo_out != nullptr && r > 0 && solo_lit < 0) {   // (the stored-like path wrote solo_out itself)
             // through LDS (the staged input is no longer needed): every wave
             // first loads a chunk of the output into LDS, then stores it from
             // LDS, so no load waits behind the stores to host memory in flight
