@@ -255,14 +255,15 @@ int lz4m_decompress_solo(const uint8_t* d_src, const int64_t* d_src_off, const i
 
 /*
  * lz4m_compress_solo: lz4m_compress_batch for ONE block of len < 65547 bytes
- * (table U16_HASH4, U32_HASH5 or AUTO), with the block staged in LDS so the
- * latency-bound lone parse reads no source byte from memory.  Same bytes as
- * the batched kernel; used by the single-call host functions below
- * (lz4m_compress_default / lz4m_compress_block_api).  LZ4M_EINVAL when len is
- * out of range.  d_src and d_out_len may live in mapped pinned host memory;
- * d_dst must be device memory; h_out: nullptr, or a mapped pinned host
- * buffer that also receives the compressed bytes at the end of the launch;
- * h_done: as for lz4m_decompress_solo.
+ * (table U16_HASH4, U32_HASH5 or AUTO), with the block staged in LDS and the
+ * compressed block assembled in LDS, so the latency-bound lone parse touches
+ * no memory.  Same bytes as the batched kernel; used by the single-call host
+ * functions below (lz4m_compress_default / lz4m_compress_block_api).
+ * LZ4M_EINVAL when len is out of range.  d_src and d_out_len may live in
+ * mapped pinned host memory; h_out: nullptr, or a mapped pinned host buffer
+ * that receives the compressed bytes at the end of the launch; d_dst (device
+ * memory) receives them instead when h_out is nullptr; h_done: as for
+ * lz4m_decompress_solo.
  */
 int lz4m_compress_solo(const uint8_t* d_src, int32_t len, uint8_t* d_dst, int32_t cap, int32_t* d_out_len,
                        int table, int acceleration, uint8_t* h_out, int32_t* h_done, lz4m_stream_t stream);
@@ -321,11 +322,13 @@ int lz4m_frame_emit(const uint8_t* d_raw, const int64_t* d_raw_off, const int32_
  * Single-buffer, HOST-pointer functions with the lz4.h contracts, for a C
  * caller replacing the reference's per-call lz4libs functions one for one
  * (lz4m_host.hip).  Synchronous.  A block of up to 64 KiB (compress: below
- * LZ4_64Klimit; decompress: input below 66 KiB) is one launch of a lone-block
- * kernel (lz4m_compress_solo / lz4m_decompress_solo) that reads the input and
- * its call record from the thread's mapped pinned staging buffer, stages the
- * block in LDS, writes the result back into that buffer itself and releases a
- * done flag the host polls: no stream copies.  Larger inputs copy to the
+ * LZ4_64Klimit; decompress: input below 66 KiB) is a request to the thread's
+ * persistent worker kernel (lz4m_single_call_worker below), or, with the
+ * worker off, one launch of a lone-block kernel (lz4m_compress_solo /
+ * lz4m_decompress_solo).  Either reads the input and its call record from
+ * the thread's mapped pinned staging buffer, stages the block in LDS, writes
+ * the result back into that buffer itself and releases a done flag the host
+ * polls: no stream copies.  Larger inputs copy to the
  * device, run the batched kernel on a batch of one and copy back (device
  * scratch cached per thread).  Throughput comes from the batched functions
  * above.

@@ -1,11 +1,13 @@
 // lz4m_host.hip -- single-buffer, host-pointer entry points with the lz4.h
 // contracts, for a C caller that replaces the
 // reference's per-call lz4libs functions one for one (e.g. a rebuilt
-// lz4/block/_block.c).  A block of up to 64 KiB is one launch of a lone-block
-// kernel on mapped pinned memory (one_block_mapped: the kernel reads the
-// caller's bytes and the call record from the thread's pinned staging buffer,
-// stages the block in LDS, writes the result back itself and releases a done
-// flag that the host polls).  Larger inputs copy to
+// lz4/block/_block.c).  A block of up to 64 KiB is a request to the thread's
+// persistent worker kernel (one_block_worker: a mailbox in coherent mapped
+// memory), or with the worker off one launch of a lone-block kernel on mapped
+// pinned memory (one_block_mapped).  Either reads the caller's bytes and the
+// call record from a pinned staging buffer, stages the block in LDS, writes
+// the result back itself and releases a done flag that the host polls
+// (DESIGN.md section 3.3b).  Larger inputs copy to
 // the device, run the batched kernel on a batch of one and copy the result
 // back; device buffers are cached per thread and grow as needed.  Throughput
 // comes from the batched entry points.
