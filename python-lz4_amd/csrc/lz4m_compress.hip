@@ -307,6 +307,23 @@ __device__ __forceinline__ void src_fetch(const Win& W, const uint8_t* w, int32_
     }
 }
 
+// LW (the whole window staged in LDS: the lone-block kernels, the LDS-staged
+// linked passes): window reads are single LDS reads at any alignment -- no
+// ring, no refills, no clamped realignment -- [p, p+16) by three aligned
+// 8-byte reads and a funnel, [p-4, p) by two aligned dwords.  The staging
+// zero-fills 64 bytes past the window, so reads past iend stay inside it.
+__device__ __forceinline__ u32x4 lw_ld16(const uint8_t* w, int32_t p) { return lds_ld16a((const lds_u8*)(w + p)); }
+__device__ __forceinline__ uint32_t lw_ld4(const uint8_t* w, int32_t p) {
+    const lds_u8* q = (const lds_u8*)(w + p);
+    const uint32_t a = lds_addr(q);
+    const lds_cu32* d = (const lds_cu32*)(q - (a & 3u));
+    return __builtin_amdgcn_alignbyte(d[1], d[0], a & 3u);
+}
+__device__ __forceinline__ uint32_t lw_before(const uint8_t* w, int32_t p) {   // as ld_before
+    const uint32_t x = lw_ld4(w, p >= 4 ? p - 4 : 0);
+    return p >= 4 ? x : p <= 0 ? 0u : x << (8 * (4 - (uint32_t)p));
+}
+
 // number of equal leading bytes of a ^ b over 12 bytes (the dwords y, z, w)
 __device__ __forceinline__ int eq12(u32x4 a, u32x4 b) {
     const uint32_t x1 = a.y ^ b.y, x2 = a.z ^ b.z, x3 = a.w ^ b.w;
@@ -333,7 +350,8 @@ __device__ __forceinline__ u32x4 readlane_x4(u32x4 v, int l) {
 // (zeroed for a fresh stream, lz4.c:1513 / LZ4_prepareTable; loaded from a
 // dictionary; or carried over from the previous block).
 // oracle: orc_compress_window (oracle/lz4_oracle.c).
-template <int V, bool ACC1 = false>
+// LW: the window w is staged in LDS (see lw_ld16); the ring is not used.
+template <int V, bool ACC1 = false, bool LW = false>
 __device__ __forceinline__ int32_t compress_block_w(const uint8_t* __restrict__ w, int32_t hist, int32_t n, uint8_t* dst,
                                     int32_t cap, int accel, uint16_t* tab, lds_u8* ring, uint32_t lane,
                                     uint32_t ibase, uint32_t low_idx, int32_t low_src, int32_t low_dict) {
@@ -363,7 +381,7 @@ __device__ __forceinline__ int32_t compress_block_w(const uint8_t* __restrict__ 
     CP_DECL
     if (n < kMinLength) goto last_literals;                    // lz4.c:981
 
-    top_up(W, w, hist + kRing, hist, lane);
+    if constexpr (!LW) top_up(W, w, hist + kRing, hist, lane);
     if (lane == 0) T::put_v(tab, T::hash(w + hist), ibase + (uint32_t)hist);   // lz4.c:984
     ip = hist + 1;
 
@@ -384,13 +402,18 @@ __device__ __forceinline__ int32_t compress_block_w(const uint8_t* __restrict__ 
                 const int32_t pos = valid ? (int32_t)pos64 : ip;
                 const uint64_t vmask = __ballot(valid);
                 const int nvalid = __builtin_popcountll(vmask);   // valid lanes are a prefix
-                if (nvalid > 0) {
-                    const int32_t pmax = __builtin_amdgcn_readlane(pos, nvalid - 1);
-                    if (pmax + 16 > W.whi) top_up(W, w, pmax + 16 + kChunk, anchor - 8, lane);
-                }
                 uint32_t pm = 0;
                 u32x4 pv = u32x4{0, 0, 0, 0};
-                src_fetch(W, w, pos, pm, pv);
+                if constexpr (LW) {
+                    pv = lw_ld16(w, pos);
+                    pm = lw_before(w, pos);
+                } else {
+                    if (nvalid > 0) {
+                        const int32_t pmax = __builtin_amdgcn_readlane(pos, nvalid - 1);
+                        if (pmax + 16 > W.whi) top_up(W, w, pmax + 16 + kChunk, anchor - 8, lane);
+                    }
+                    src_fetch(W, w, pos, pm, pv);
+                }
                 CP_COUNT(8, 1);
                 CP_COUNT(15, __builtin_popcountll(__ballot(valid && !W.has(pos - 4, 20))));
                 const uint32_t cur = ibase + (uint32_t)pos;
@@ -433,11 +456,16 @@ __device__ __forceinline__ int32_t compress_block_w(const uint8_t* __restrict__ 
                 ok = valid && !((T::kDistCheck && cand + 65535u < cur) || cand < low_idx);
                 if (ok) cpos = (int32_t)cand - (int32_t)ibase;
                 // refill the ring ahead of the parse under the same wait
-                const bool pf = W.whi < ip + (kRing - kChunk) && can_fill(W, anchor - 8);
+                const bool pf = !LW && W.whi < ip + (kRing - kChunk) && can_fill(W, anchor - 8);
                 u32x4 fv = u32x4{0, 0, 0, 0};
                 if (pf) fv = fill_load(W, w, lane);
-                gv = ld16_win(w, cpos, iend);   // unconditional (cpos = pos when not ok)
-                gm = ld_before(w, cpos);
+                if constexpr (LW) {
+                    gv = lw_ld16(w, cpos);
+                    gm = lw_before(w, cpos);
+                } else {
+                    gv = ld16_win(w, cpos, iend);   // unconditional (cpos = pos when not ok)
+                    gm = ld_before(w, cpos);
+                }
                 const bool hit = ok && gv.x == pv.x;
                 const uint64_t hmask = __ballot(hit);
                 const int f = hmask ? __builtin_ctzll(hmask) : nvalid;   // last lane processed: f (or all valid)
@@ -505,11 +533,16 @@ __device__ __forceinline__ int32_t compress_block_w(const uint8_t* __restrict__ 
                 const int32_t q = b0 + 16 * (int32_t)lane;
                 if (q < lit) {
                     const int32_t p = anchor + q;
-                    const bool in = W.has(p, 16);
-                    u32x4 v = ring_fetch16(W, p);
-                    if (__any(!in)) {
-                        const u32x4 gv = ld16_win(w, p, iend);
-                        if (!in) v = gv;
+                    u32x4 v;
+                    if constexpr (LW) {
+                        v = lw_ld16(w, p);
+                    } else {
+                        const bool in = W.has(p, 16);
+                        v = ring_fetch16(W, p);
+                        if (__any(!in)) {
+                            const u32x4 gv = ld16_win(w, p, iend);
+                            if (!in) v = gv;
+                        }
                     }
                     if (lit - q >= 16 || d_room - q >= 16) {
                         st16(d + q, v);
@@ -592,10 +625,15 @@ __device__ __forceinline__ int32_t compress_block_w(const uint8_t* __restrict__ 
         if (ip >= mflimit1) break;                             // lz4.c:1204
 
         {   // ---- fill table, test next position (lz4.c:1207-1258) ----
-            if (ip + 16 > W.whi) top_up(W, w, ip + 16 + kChunk, ip - 8, lane);
             uint32_t pm;
             u32x4 pv;
-            src_fetch(W, w, ip, pm, pv);
+            if constexpr (LW) {
+                pv = lw_ld16(w, ip);
+                pm = lw_before(w, ip);
+            } else {
+                if (ip + 16 > W.whi) top_up(W, w, ip + 16 + kChunk, ip - 8, lane);
+                src_fetch(W, w, ip, pm, pv);
+            }
             // bytes [ip-2, ip+6)
             const u32x4 pv2 = u32x4{__builtin_amdgcn_alignbyte(pv.x, pm, 2), __builtin_amdgcn_alignbyte(pv.y, pv.x, 2),
                                     0u, 0u};
@@ -608,7 +646,7 @@ __device__ __forceinline__ int32_t compress_block_w(const uint8_t* __restrict__ 
             const bool ok = cand >= low_idx && (!T::kDistCheck || cand + 65535u >= cur);
             {
                 const int32_t cpos = ok ? (int32_t)cand - (int32_t)ibase : ip;
-                const u32x4 gv = ld16_win(w, cpos, iend);
+                const u32x4 gv = LW ? lw_ld16(w, cpos) : ld16_win(w, cpos, iend);
                 if (ok && gv.x == pv.x) {
                     match = cpos;
                     P = pv;
@@ -657,13 +695,13 @@ __device__ __forceinline__ void zero_table(uint16_t* tab, uint32_t lane) {
 }
 
 // One block with a fresh table (LZ4_compress_generic_validated, noDict).
-template <int V, bool ACC1>
+template <int V, bool ACC1, bool LW = false>
 __device__ __forceinline__ int64_t compress_block(const uint8_t* __restrict__ src, int64_t n, uint8_t* dst,
                                                   int64_t cap, int accel, uint16_t* tab, lds_u8* ring,
                                                   uint32_t lane) {
     if (n > kMaxInput) return 0;
     zero_table(tab, lane);
-    return compress_block_w<V, ACC1>(src, 0, n, dst, cap, accel, tab, ring, lane, 0u, 0u, 0, 0);
+    return compress_block_w<V, ACC1, LW>(src, 0, n, dst, cap, accel, tab, ring, lane, 0u, 0u, 0, 0);
 }
 
 // `only`: -1 every block; 0 only blocks < 65547 B; 1 only blocks >= 65547 B.
@@ -733,8 +771,8 @@ __device__ __forceinline__ void compress_solo_body(const uint8_t* __restrict__ s
         // a capacity at or above the bound parses as "not limited" whatever its
         // size (lz4.c:1330-1343), so the bound is the LDS output's size
         const int32_t bound = len + len / 255 + 16;
-        const int64_t r = compress_block<V, ACC1>((const uint8_t*)blk, len, obuf, cap < bound ? cap : bound, accel,
-                                                  tab, ring, t);
+        const int64_t r = compress_block<V, ACC1, true>((const uint8_t*)blk, len, obuf, cap < bound ? cap : bound,
+                                                        accel, tab, ring, t);
         if (t == 0) {
             *out_len = (int32_t)r;
             solo_r = (int32_t)r;
@@ -1045,8 +1083,8 @@ __global__ __launch_bounds__(256) void compress_spec_lds_kernel(
         // waits for the wave's stores in flight)
         int64_t r;
         if (staged)
-            r = compress_block_w<LZ4M_TABLE_U32_HASH5>((const uint8_t*)win, hist, len, dst + dst_off[b], dst_cap[b],
-                                                       accel, tab, ring, lane, 0u, 0u, 0, 0);
+            r = compress_block_w<LZ4M_TABLE_U32_HASH5, false, true>((const uint8_t*)win, hist, len, dst + dst_off[b],
+                                                                    dst_cap[b], accel, tab, ring, lane, 0u, 0u, 0, 0);
         else
             r = compress_block_w<LZ4M_TABLE_U32_HASH5>(wg, hist, len, dst + dst_off[b], dst_cap[b], accel, tab, ring,
                                                        lane, 0u, 0u, 0, 0);

@@ -39,3 +39,22 @@ for kind in os.environ.get("KINDS", "silesia").split(","):
           f"global-fetch lanes {v[15]}")
     print(f"  wave-cycles per sequence {tot / seq:.0f}: " +
           ", ".join(f"{PH[i]} {v[i] / seq:.0f}" for i in PH))
+
+if os.environ.get("SINGLE"):
+    # the single-call path (persistent worker, LDS-staged block) on config 1's random blocks
+    import random
+    rnd = random.Random(12345)
+    blocks = [rnd.randbytes(65536) for _ in range(200)]
+    out = C.create_string_buffer(70000)
+    for b in blocks[:20]:
+        lib.lz4m_compress_default(b, out, 65536, 70000)
+    buf = (C.c_ulonglong * 32)()
+    lib.lz4m_compress_prof(buf, 1)
+    for b in blocks:
+        lib.lz4m_compress_default(b, out, 65536, 70000)
+    lib.lz4m_compress_prof(buf, 1)
+    v = list(buf)
+    n = len(blocks)
+    print(f"single-call random 64 KiB: per call {sum(v[i] for i in PH) / n:.0f} wave-cycles, search steps "
+          f"{v[8] / n:.1f}, group iters {v[11] / n:.1f}, global-fetch lanes {v[15] / n:.1f}; " +
+          ", ".join(f"{PH[i]} {v[i] / n:.0f}" for i in PH))
