@@ -351,10 +351,16 @@ __device__ __forceinline__ u32x4 readlane_x4(u32x4 v, int l) {
 // dictionary; or carried over from the previous block).
 // oracle: orc_compress_window (oracle/lz4_oracle.c).
 // LW: the window w is staged in LDS (see lw_ld16); the ring is not used.
+// last_lit (nullptr, or LDS): the last literals are NOT copied; lane 0 stores
+// {their output offset, their window offset} there for the caller to copy
+// (the lone-block kernel copies them straight from the staged block to the
+// host with all four waves: one wave copying 64 KiB inside LDS was 25 % of a
+// random block's call).
 template <int V, bool ACC1 = false, bool LW = false>
 __device__ __forceinline__ int32_t compress_block_w(const uint8_t* __restrict__ w, int32_t hist, int32_t n, uint8_t* dst,
                                     int32_t cap, int accel, uint16_t* tab, lds_u8* ring, uint32_t lane,
-                                    uint32_t ibase, uint32_t low_idx, int32_t low_src, int32_t low_dict) {
+                                    uint32_t ibase, uint32_t low_idx, int32_t low_src, int32_t low_dict,
+                                    int32_t* last_lit = nullptr) {
     using T = Table<V>;
     if (n > kMaxInput) return 0;                               // lz4.c:1324
     const bool limited = cap < bound64(n);
@@ -679,7 +685,14 @@ last_literals:
         } else if (lane == 0) {
             dst[tpos] = (uint8_t)(run << 4);
         }
-        wave_copy(dst + op, w + anchor, run, cap - op, iend - anchor, lane);
+        if (last_lit != nullptr) {
+            if (lane == 0) {
+                last_lit[0] = op;
+                last_lit[1] = anchor;
+            }
+        } else {
+            wave_copy(dst + op, w + anchor, run, cap - op, iend - anchor, lane);
+        }
         op += run;
     }
     CP_MARK(7);
@@ -698,10 +711,10 @@ __device__ __forceinline__ void zero_table(uint16_t* tab, uint32_t lane) {
 template <int V, bool ACC1, bool LW = false>
 __device__ __forceinline__ int64_t compress_block(const uint8_t* __restrict__ src, int64_t n, uint8_t* dst,
                                                   int64_t cap, int accel, uint16_t* tab, lds_u8* ring,
-                                                  uint32_t lane) {
+                                                  uint32_t lane, int32_t* last_lit = nullptr) {
     if (n > kMaxInput) return 0;
     zero_table(tab, lane);
-    return compress_block_w<V, ACC1, LW>(src, 0, n, dst, cap, accel, tab, ring, lane, 0u, 0u, 0, 0);
+    return compress_block_w<V, ACC1, LW>(src, 0, n, dst, cap, accel, tab, ring, lane, 0u, 0u, 0, 0, last_lit);
 }
 
 // `only`: -1 every block; 0 only blocks < 65547 B; 1 only blocks >= 65547 B.
@@ -745,7 +758,7 @@ template <int V, bool ACC1>
 __device__ __forceinline__ void compress_solo_body(const uint8_t* __restrict__ src, int32_t len, uint8_t* dst,
                                                    int32_t cap, int32_t* __restrict__ out_len, int accel,
                                                    uint8_t* h_out, int32_t* h_done, uint8_t* blk, uint8_t* obuf,
-                                                   uint16_t* tab, lds_u8* ring, int32_t& solo_r) {
+                                                   uint16_t* tab, lds_u8* ring, int32_t& solo_r, int32_t* last_lit) {
     const uint32_t t = threadIdx.x;
     constexpr int kStep = 16 * 256;
     const int32_t lim = len + 64 < kSoloBuf ? len + 64 : kSoloBuf;   // the block and 64 zero bytes
@@ -767,12 +780,13 @@ __device__ __forceinline__ void compress_solo_body(const uint8_t* __restrict__ s
     }
     __syncthreads();
     LZ4M_WTS(ts, 1);
+    if (t == 0) last_lit[0] = -1;
     if (t < kWave) {
         // a capacity at or above the bound parses as "not limited" whatever its
         // size (lz4.c:1330-1343), so the bound is the LDS output's size
         const int32_t bound = len + len / 255 + 16;
         const int64_t r = compress_block<V, ACC1, true>((const uint8_t*)blk, len, obuf, cap < bound ? cap : bound,
-                                                        accel, tab, ring, t);
+                                                        accel, tab, ring, t, last_lit);
         if (t == 0) {
             *out_len = (int32_t)r;
             solo_r = (int32_t)r;
@@ -781,15 +795,30 @@ __device__ __forceinline__ void compress_solo_body(const uint8_t* __restrict__ s
     __syncthreads();
     LZ4M_WTS(ts, 2);
     // the compressed bytes from LDS to the caller's mapped host buffer (or to
-    // dst), all four waves: LDS reads and stores only, nothing waits on a store
+    // dst), all four waves: LDS reads and stores only, nothing waits on a
+    // store.  The last literals come straight from the staged block.
     const int32_t r = solo_r;
     uint8_t* out = h_out != nullptr ? h_out : dst;
-    for (int32_t p = 16 * (int32_t)t; p < r; p += kStep) {
+    const int32_t split = r > 0 && last_lit[0] >= 0 ? last_lit[0] : r;   // [0, split) in obuf
+    for (int32_t p = 16 * (int32_t)t; p < split; p += kStep) {
         const u32x4 v = lds_ld16((const lds_u8*)obuf + p);
-        if (p + 16 <= r) {
+        if (p + 16 <= split) {
             st16(out + p, v);
         } else {
-            for (int32_t k = p; k < r; ++k) out[k] = obuf[k];
+            for (int32_t k = p; k < split; ++k) out[k] = obuf[k];
+        }
+    }
+    if (split < r) {
+        const lds_u8* lit = (const lds_u8*)blk + last_lit[1];
+        uint8_t* o = out + split;
+        const int32_t m = r - split;
+        for (int32_t p = 16 * (int32_t)t; p < m; p += kStep) {
+            const u32x4 v = lds_ld16a(lit + p);
+            if (p + 16 <= m) {
+                st16(o + p, v);
+            } else {
+                for (int32_t j = 0; j < m - p; ++j) o[p + j] = (uint8_t)byte_of(v, (int)j);
+            }
         }
     }
     if (h_done != nullptr) {   // all of the above visible to the host, then the flag it polls
@@ -1125,12 +1154,13 @@ template <int V, bool ACC1>
 __global__ __launch_bounds__(256) void compress_solo_kernel(const uint8_t* __restrict__ src, int32_t len,
                                                             uint8_t* dst, int32_t cap, int32_t* __restrict__ out_len,
                                                             int accel, uint8_t* h_out, int32_t* h_done) {
-    __shared__ int32_t solo_r;
+    __shared__ int32_t solo_r, last_lit[2];
     __shared__ __attribute__((aligned(16))) uint8_t blk[kSoloBuf];
     __shared__ __attribute__((aligned(16))) uint8_t obuf[kSoloOut];
     __shared__ __attribute__((aligned(16))) uint16_t tab[8192];
     RING_DECL
-    compress_solo_body<V, ACC1>(src, len, dst, cap, out_len, accel, h_out, h_done, blk, obuf, tab, ring, solo_r);
+    compress_solo_body<V, ACC1>(src, len, dst, cap, out_len, accel, h_out, h_done, blk, obuf, tab, ring, solo_r,
+                                last_lit);
 }
 
 // The single-call compress worker (lz4m_worker.h): one persistent workgroup
@@ -1138,7 +1168,7 @@ __global__ __launch_bounds__(256) void compress_solo_kernel(const uint8_t* __res
 // the LDS buffers are declared once here and shared by every table variant.
 __global__ __launch_bounds__(256) void compress_worker(Mailbox* mb, uint8_t* hd, uint8_t* dbuf, uint64_t idle) {
     __shared__ uint32_t cmd[8];
-    __shared__ int32_t solo_r;
+    __shared__ int32_t solo_r, last_lit[2];
     __shared__ __attribute__((aligned(16))) uint8_t blk[kSoloBuf];
     __shared__ __attribute__((aligned(16))) uint8_t obuf[kSoloOut];
     __shared__ __attribute__((aligned(16))) uint16_t tab[8192];
@@ -1156,17 +1186,17 @@ __global__ __launch_bounds__(256) void compress_worker(Mailbox* mb, uint8_t* hd,
         if (table == LZ4M_TABLE_U32_HASH5) {
             if (accel == 1)
                 compress_solo_body<LZ4M_TABLE_U32_HASH5, true>(hd, len, dbuf, cap, &rec->result, accel, hout, &rec->done,
-                                                              blk, obuf, tab, ring, solo_r);
+                                                              blk, obuf, tab, ring, solo_r, last_lit);
             else
                 compress_solo_body<LZ4M_TABLE_U32_HASH5, false>(hd, len, dbuf, cap, &rec->result, accel, hout,
-                                                               &rec->done, blk, obuf, tab, ring, solo_r);
+                                                               &rec->done, blk, obuf, tab, ring, solo_r, last_lit);
         } else {   // AUTO / U16: below 65547 bytes the byU16 parse (lz4.c:1352-1357)
             if (accel == 1)
                 compress_solo_body<LZ4M_TABLE_U16_HASH4, true>(hd, len, dbuf, cap, &rec->result, accel, hout, &rec->done,
-                                                              blk, obuf, tab, ring, solo_r);
+                                                              blk, obuf, tab, ring, solo_r, last_lit);
             else
                 compress_solo_body<LZ4M_TABLE_U16_HASH4, false>(hd, len, dbuf, cap, &rec->result, accel, hout,
-                                                               &rec->done, blk, obuf, tab, ring, solo_r);
+                                                               &rec->done, blk, obuf, tab, ring, solo_r, last_lit);
         }
     }
 }
