@@ -324,6 +324,23 @@ __device__ __forceinline__ uint32_t lw_before(const uint8_t* w, int32_t p) {   /
     return p >= 4 ? x : p <= 0 ? 0u : x << (8 * (4 - (uint32_t)p));
 }
 
+// LW with `stage` (the lone-block kernel): the window is still being staged
+// by the other waves, kStageChunk bytes at a time, and stage[c] != 0 once
+// chunk c is in LDS.  lw_need(x) waits until bytes [0, x) are; `have` (wave
+// uniform) is what the parse already knows to be staged.
+constexpr int32_t kStageChunk = 4096;
+typedef __attribute__((address_space(3))) volatile int32_t lds_vi32;
+__device__ __forceinline__ void lw_need(const int32_t* stage, int32_t& have, int32_t x) {
+    if (stage == nullptr) return;
+    while (have < x) {
+        const lds_vi32* f = (const lds_vi32*)stage;
+        const int32_t c = have / kStageChunk;
+        for (uint32_t spins = 0; f[c] == 0 && spins < (1u << 22); ++spins) __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        have += kStageChunk;
+    }
+}
+
 // number of equal leading bytes of a ^ b over 12 bytes (the dwords y, z, w)
 __device__ __forceinline__ int eq12(u32x4 a, u32x4 b) {
     const uint32_t x1 = a.y ^ b.y, x2 = a.z ^ b.z, x3 = a.w ^ b.w;
@@ -360,7 +377,7 @@ template <int V, bool ACC1 = false, bool LW = false>
 __device__ __forceinline__ int32_t compress_block_w(const uint8_t* __restrict__ w, int32_t hist, int32_t n, uint8_t* dst,
                                     int32_t cap, int accel, uint16_t* tab, lds_u8* ring, uint32_t lane,
                                     uint32_t ibase, uint32_t low_idx, int32_t low_src, int32_t low_dict,
-                                    int32_t* last_lit = nullptr) {
+                                    int32_t* last_lit = nullptr, const int32_t* stage = nullptr) {
     using T = Table<V>;
     if (n > kMaxInput) return 0;                               // lz4.c:1324
     const bool limited = cap < bound64(n);
@@ -384,10 +401,12 @@ __device__ __forceinline__ int32_t compress_block_w(const uint8_t* __restrict__ 
     u32x4 P, G;
     int32_t pbase = 0, gbase = 0, back = 0;
 
+    int32_t staged = 0;   // LW with `stage`: bytes known to be in LDS (wave uniform)
     CP_DECL
     if (n < kMinLength) goto last_literals;                    // lz4.c:981
 
     if constexpr (!LW) top_up(W, w, hist + kRing, hist, lane);
+    if constexpr (LW) lw_need(stage, staged, hist + 8);
     if (lane == 0) T::put_v(tab, T::hash(w + hist), ibase + (uint32_t)hist);   // lz4.c:984
     ip = hist + 1;
 
@@ -411,6 +430,8 @@ __device__ __forceinline__ int32_t compress_block_w(const uint8_t* __restrict__ 
                 uint32_t pm = 0;
                 u32x4 pv = u32x4{0, 0, 0, 0};
                 if constexpr (LW) {
+                    if (stage != nullptr && nvalid > 0)
+                        lw_need(stage, staged, __builtin_amdgcn_readlane(pos, nvalid - 1) + 24);
                     pv = lw_ld16(w, pos);
                     pm = lw_before(w, pos);
                 } else {
@@ -580,6 +601,10 @@ __device__ __forceinline__ int32_t compress_block_w(const uint8_t* __restrict__ 
                 int32_t more = 0;
                 const int32_t p = pbase + 16, q = gbase + 16;
                 for (;;) {
+                    if constexpr (LW) {   // the compares read no further than matchlimit
+                        const int32_t x = p + more + 4 * kWave + 8;
+                        lw_need(stage, staged, x < iend ? x : iend);
+                    }
                     const int32_t av = matchlimit - (p + more);
                     const int32_t at = more + 4 * (int32_t)lane;
                     const int32_t rem = av - 4 * (int32_t)lane;   // bytes this lane may compare
@@ -634,6 +659,7 @@ __device__ __forceinline__ int32_t compress_block_w(const uint8_t* __restrict__ 
             uint32_t pm;
             u32x4 pv;
             if constexpr (LW) {
+                lw_need(stage, staged, ip + 24);
                 pv = lw_ld16(w, ip);
                 pm = lw_before(w, ip);
             } else {
@@ -711,10 +737,12 @@ __device__ __forceinline__ void zero_table(uint16_t* tab, uint32_t lane) {
 template <int V, bool ACC1, bool LW = false>
 __device__ __forceinline__ int64_t compress_block(const uint8_t* __restrict__ src, int64_t n, uint8_t* dst,
                                                   int64_t cap, int accel, uint16_t* tab, lds_u8* ring,
-                                                  uint32_t lane, int32_t* last_lit = nullptr) {
+                                                  uint32_t lane, int32_t* last_lit = nullptr,
+                                                  const int32_t* stage = nullptr) {
     if (n > kMaxInput) return 0;
     zero_table(tab, lane);
-    return compress_block_w<V, ACC1, LW>(src, 0, n, dst, cap, accel, tab, ring, lane, 0u, 0u, 0, 0, last_lit);
+    return compress_block_w<V, ACC1, LW>(src, 0, n, dst, cap, accel, tab, ring, lane, 0u, 0u, 0, 0, last_lit,
+                                         stage);
 }
 
 // `only`: -1 every block; 0 only blocks < 65547 B; 1 only blocks >= 65547 B.
@@ -753,40 +781,52 @@ constexpr int kSoloMax = kLimit64K - 1;                  // the U16 table's rang
 constexpr int kSoloBuf = ((kSoloMax + 64) + 15) & ~15;   // + zero padding past the block
 constexpr int kSoloBound = kSoloMax + kSoloMax / 255 + 16;          // LZ4_compressBound(kSoloMax)
 constexpr int kSoloOut = ((kSoloBound + 15) & ~15) + 64;            // + room for 16-byte wild stores
-constexpr int kSoloU = 4;   // 16-byte pieces in flight per lane when staging
+constexpr int kSoloU = 4;   // 16-byte pieces in flight per lane when staging (16 x 64 lanes x 4 = one 4 KiB chunk)
+static_assert(16 * 64 * kSoloU == kStageChunk, "a staging round is one chunk");
 template <int V, bool ACC1>
 __device__ __forceinline__ void compress_solo_body(const uint8_t* __restrict__ src, int32_t len, uint8_t* dst,
                                                    int32_t cap, int32_t* __restrict__ out_len, int accel,
                                                    uint8_t* h_out, int32_t* h_done, uint8_t* blk, uint8_t* obuf,
-                                                   uint16_t* tab, lds_u8* ring, int32_t& solo_r, int32_t* last_lit) {
+                                                   uint16_t* tab, lds_u8* ring, int32_t& solo_r, int32_t* last_lit,
+                                                   int32_t* stage) {
     const uint32_t t = threadIdx.x;
     constexpr int kStep = 16 * 256;
     const int32_t lim = len + 64 < kSoloBuf ? len + 64 : kSoloBuf;   // the block and 64 zero bytes
     uint32_t* ts = h_done ? reinterpret_cast<uint32_t*>(h_done + 1) : nullptr;   // CallMeta::work (LZ4M_WORKER_TS)
     (void)ts;
     LZ4M_WTS(ts, 0);
-    for (int32_t base = 0; base < lim; base += kSoloU * kStep) {   // four pieces in flight per lane (16 measured no faster over PCIe)
-        u32x4 v[kSoloU];
-#pragma unroll
-        for (int u = 0; u < kSoloU; ++u) {
-            const int32_t p = base + u * kStep + 16 * (int32_t)t;
-            v[u] = p + 16 <= len ? ld16(src + p) : ld16_guarded(src + p, len - p);
-        }
-#pragma unroll
-        for (int u = 0; u < kSoloU; ++u) {
-            const int32_t p = base + u * kStep + 16 * (int32_t)t;
-            if (p < lim) lds_st16((lds_u8*)blk + p, v[u]);
-        }
-    }
-    __syncthreads();
-    LZ4M_WTS(ts, 1);
+    // Waves 1-3 stage the block in 4 KiB chunks (chunk c by wave 1 + c % 3,
+    // four 16-byte pieces per lane in flight), each flagged in `stage` once in
+    // LDS; wave 0 zeroes the table and parses meanwhile, waiting for a chunk
+    // only when it reaches it (lw_need): the PCIe staging overlaps the parse.
+    constexpr int kStages = (kSoloBuf + kStageChunk - 1) / kStageChunk;
+    if (t < kStages) stage[t] = 0;
     if (t == 0) last_lit[0] = -1;
-    if (t < kWave) {
+    __syncthreads();
+    const uint32_t wv = t >> 6, ln = t & 63;
+    if (wv >= 1) {
+        for (int32_t c = (int32_t)wv - 1; c * kStageChunk < lim; c += 3) {
+            u32x4 v[kSoloU];
+#pragma unroll
+            for (int u = 0; u < kSoloU; ++u) {
+                const int32_t p = c * kStageChunk + u * 16 * kWave + 16 * (int32_t)ln;
+                v[u] = p + 16 <= len ? ld16(src + p) : ld16_guarded(src + p, len - p);
+            }
+#pragma unroll
+            for (int u = 0; u < kSoloU; ++u) {
+                const int32_t p = c * kStageChunk + u * 16 * kWave + 16 * (int32_t)ln;
+                if (p < lim) lds_st16((lds_u8*)blk + p, v[u]);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (ln == 0) *(lds_vi32*)(stage + c) = 1;
+        }
+    } else {
+        LZ4M_WTS(ts, 1);
         // a capacity at or above the bound parses as "not limited" whatever its
         // size (lz4.c:1330-1343), so the bound is the LDS output's size
         const int32_t bound = len + len / 255 + 16;
         const int64_t r = compress_block<V, ACC1, true>((const uint8_t*)blk, len, obuf, cap < bound ? cap : bound,
-                                                        accel, tab, ring, t, last_lit);
+                                                        accel, tab, ring, t, last_lit, stage);
         if (t == 0) {
             *out_len = (int32_t)r;
             solo_r = (int32_t)r;
@@ -1154,13 +1194,13 @@ template <int V, bool ACC1>
 __global__ __launch_bounds__(256) void compress_solo_kernel(const uint8_t* __restrict__ src, int32_t len,
                                                             uint8_t* dst, int32_t cap, int32_t* __restrict__ out_len,
                                                             int accel, uint8_t* h_out, int32_t* h_done) {
-    __shared__ int32_t solo_r, last_lit[2];
+    __shared__ int32_t solo_r, last_lit[2], stage[(kSoloBuf + kStageChunk - 1) / kStageChunk];
     __shared__ __attribute__((aligned(16))) uint8_t blk[kSoloBuf];
     __shared__ __attribute__((aligned(16))) uint8_t obuf[kSoloOut];
     __shared__ __attribute__((aligned(16))) uint16_t tab[8192];
     RING_DECL
     compress_solo_body<V, ACC1>(src, len, dst, cap, out_len, accel, h_out, h_done, blk, obuf, tab, ring, solo_r,
-                                last_lit);
+                                last_lit, stage);
 }
 
 // The single-call compress worker (lz4m_worker.h): one persistent workgroup
@@ -1168,7 +1208,7 @@ __global__ __launch_bounds__(256) void compress_solo_kernel(const uint8_t* __res
 // the LDS buffers are declared once here and shared by every table variant.
 __global__ __launch_bounds__(256) void compress_worker(Mailbox* mb, uint8_t* hd, uint8_t* dbuf, uint64_t idle) {
     __shared__ uint32_t cmd[8];
-    __shared__ int32_t solo_r, last_lit[2];
+    __shared__ int32_t solo_r, last_lit[2], stage[(kSoloBuf + kStageChunk - 1) / kStageChunk];
     __shared__ __attribute__((aligned(16))) uint8_t blk[kSoloBuf];
     __shared__ __attribute__((aligned(16))) uint8_t obuf[kSoloOut];
     __shared__ __attribute__((aligned(16))) uint16_t tab[8192];
@@ -1186,17 +1226,17 @@ __global__ __launch_bounds__(256) void compress_worker(Mailbox* mb, uint8_t* hd,
         if (table == LZ4M_TABLE_U32_HASH5) {
             if (accel == 1)
                 compress_solo_body<LZ4M_TABLE_U32_HASH5, true>(hd, len, dbuf, cap, &rec->result, accel, hout, &rec->done,
-                                                              blk, obuf, tab, ring, solo_r, last_lit);
+                                                              blk, obuf, tab, ring, solo_r, last_lit, stage);
             else
                 compress_solo_body<LZ4M_TABLE_U32_HASH5, false>(hd, len, dbuf, cap, &rec->result, accel, hout,
-                                                               &rec->done, blk, obuf, tab, ring, solo_r, last_lit);
+                                                               &rec->done, blk, obuf, tab, ring, solo_r, last_lit, stage);
         } else {   // AUTO / U16: below 65547 bytes the byU16 parse (lz4.c:1352-1357)
             if (accel == 1)
                 compress_solo_body<LZ4M_TABLE_U16_HASH4, true>(hd, len, dbuf, cap, &rec->result, accel, hout, &rec->done,
-                                                              blk, obuf, tab, ring, solo_r, last_lit);
+                                                              blk, obuf, tab, ring, solo_r, last_lit, stage);
             else
                 compress_solo_body<LZ4M_TABLE_U16_HASH4, false>(hd, len, dbuf, cap, &rec->result, accel, hout,
-                                                               &rec->done, blk, obuf, tab, ring, solo_r, last_lit);
+                                                               &rec->done, blk, obuf, tab, ring, solo_r, last_lit, stage);
         }
     }
 }
