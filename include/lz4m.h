@@ -382,6 +382,15 @@ uint32_t lz4m_xxh32_host(const void* input, size_t length, uint32_t seed);
  * lone-block kernel per call), -1 = query.  Returns the previous mode. */
 int lz4m_single_call_worker(int mode);
 
+/* Diagnostics of the calling thread's workers (tests, tools/probe_worker.py):
+ * out[0..7] = decompress / compress mailbox seq, served, quit, and the two
+ * launched flags; out[8..11] = per kind the requests its last launch served
+ * and how that launch ended (1 idle, 2 quit); out[12..15] = per kind the
+ * poll's real-time stamps (LZ4M_WORKER_TS builds).  Returns the number of
+ * requests a worker neither served nor gave up within 1 s (each one turned
+ * the worker off).  Host memory only: no HIP call. */
+int lz4m_single_call_worker_state(uint32_t out[16]);
+
 /* Host memcpy of n bytes split over `threads` threads (1..16; one below
  * 4 MiB); when `hash` is not NULL, one more thread runs
  * lz4m_xxh32_host_update(hash, src, n) over the same source meanwhile.  The

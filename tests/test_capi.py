@@ -186,3 +186,22 @@ def test_host_xxh32_matches_oracle_and_golden():
         assert N.xxh32_host(data, e.get("seed", 0)) == e["value"], e
         checked += 1
     assert checked > 0
+
+
+def test_single_call_worker_controls_without_gpu():
+    """lz4m_single_call_worker switches and reports the single-call mode, and
+    lz4m_single_call_worker_state reads this thread's (never started) workers:
+    neither makes a HIP call, so both work without a GPU."""
+    from lz4 import _native as N
+    lib = N.lib()
+    prev = lib.lz4m_single_call_worker(-1)
+    assert prev in (0, 1)
+    try:
+        assert lib.lz4m_single_call_worker(1) == prev
+        assert lib.lz4m_single_call_worker(-1) == 1
+        assert lib.lz4m_single_call_worker(7) == 1       # not a mode: query only
+        st = (C.c_uint32 * 16)()
+        assert lib.lz4m_single_call_worker_state(st) == 0
+        assert list(st) == [0] * 16
+    finally:
+        lib.lz4m_single_call_worker(prev)
