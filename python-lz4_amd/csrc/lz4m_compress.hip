@@ -678,6 +678,7 @@ __device__ __forceinline__ int32_t compress_block_w(const uint8_t* __restrict__ 
             const bool ok = cand >= low_idx && (!T::kDistCheck || cand + 65535u >= cur);
             {
                 const int32_t cpos = ok ? (int32_t)cand - (int32_t)ibase : ip;
+                // (a candidate inside the ring read from there instead: -0.5 %, r04aa)
                 const u32x4 gv = LW ? lw_ld16(w, cpos) : ld16_win(w, cpos, iend);
                 if (ok && gv.x == pv.x) {
                     match = cpos;
