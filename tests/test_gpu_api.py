@@ -696,3 +696,42 @@ def test_single_call_decompress_golden_and_mutated(gpu, golden, oracle, single_c
         assert got == st, (len(src), cap)
         if st > 0:
             assert out.raw[:st] == want[:st]
+
+
+def test_single_call_many_threads(gpu, oracle):
+    """Single calls from several host threads at once (each thread has its own
+    staging buffers; the workers are served in turn): every result equals the
+    oracle's and no call waits on another thread's persistent kernel."""
+    import threading
+    import time
+    import lz4.block
+    rng = np.random.default_rng(77)
+    blocks = [rng.integers(0, 256, 65536, dtype=np.uint8).tobytes() if i % 3 == 0 else
+              bytes(rng.integers(0, 4, 65536, dtype=np.uint8)) for i in range(24)]
+    from oracle import TABLE_U32_HASH5
+    want = [oracle.compress(b, variant=TABLE_U32_HASH5) for b in blocks]   # lz4.block.compress: byU32 / hash5
+    errors, times = [], []
+
+    def work(k):
+        t0 = time.perf_counter()
+        for rep in range(6):
+            for i in range(k, len(blocks), 4):
+                c = lz4.block.compress(blocks[i], store_size=False)
+                if c != want[i]:
+                    errors.append(("compress", k, i))
+                if lz4.block.decompress(c, uncompressed_size=65536) != blocks[i]:
+                    errors.append(("decompress", k, i))
+        times.append(time.perf_counter() - t0)
+
+    ts = [threading.Thread(target=work, args=(k,)) for k in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=120)
+    assert not any(t.is_alive() for t in ts)
+    assert not errors, errors[:5]
+    assert max(times) < 5.0, times   # 36 round trips per thread: milliseconds, not a stalled worker's seconds
+    import ctypes as C
+    import lz4._native as N
+    st = (C.c_uint32 * 16)()
+    assert N.lib().lz4m_single_call_worker_state(st) == 0   # no worker missed its 1 s deadline (none turned off)
