@@ -1113,6 +1113,7 @@ __global__ __launch_bounds__(256) void compress_spec_lds_kernel(
     u32x4* t4 = reinterpret_cast<u32x4*>(tab);
     const uint32_t t = threadIdx.x, lane = t & 63;
     const int64_t b = list[blockIdx.x];   // linked, b >= 1, its predecessor's table changed
+    if (b < 1 || b >= n) return;           // (the host sized the grid from the same count; never taken)
     const bool feeds = b + 1 < n && link[b + 1] != 0;
     const int32_t len = src_len[b];
     if (src_len[b - 1] < (int32_t)kWin) {   // speculation needs >= 64 KiB predecessors (as compress_spec_kernel)
