@@ -41,3 +41,21 @@ for name, f in cases.items():
     for _ in range(500):
         f()
     print(f"{name}: {(time.perf_counter() - t) / 500 * 1e6:.1f} us per call")
+
+# the same calls on compressible data (silesia-like mix, lz4/_synth.py)
+if os.environ.get("C1_SYNTH", "1") == "1":
+    import numpy as np  # noqa: E402
+    from lz4 import _synth  # noqa: E402
+    for kind in ("silesia", "text", "records"):
+        sb = [bytes(x) for x in _synth.blocks(64, kind, seed=5)]
+        sc = [B.compress(b) for b in sb]
+        for rep in range(2):
+            t = time.perf_counter()
+            sc = [B.compress(b) for b in sb]
+            tc = (time.perf_counter() - t) / len(sb)
+            t = time.perf_counter()
+            back = [B.decompress(c) for c in sc]
+            td = (time.perf_counter() - t) / len(sb)
+        assert back == sb
+        ratio = sum(map(len, sb)) / sum(map(len, sc))
+        print(f"{kind} (ratio {ratio:.2f}): per call compress {tc * 1e6:.1f} us, decompress {td * 1e6:.1f} us")
