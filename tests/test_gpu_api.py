@@ -735,3 +735,21 @@ def test_single_call_many_threads(gpu, oracle):
     import lz4._native as N
     st = (C.c_uint32 * 16)()
     assert N.lib().lz4m_single_call_worker_state(st) == 0   # no worker missed its 1 s deadline (none turned off)
+
+
+@pytest.mark.parametrize("size", [(40 << 20) + 12345, (96 << 20) + 7])
+def test_frame_dropin_large_odd_sizes(gpu, reference, size):
+    """lz4.frame.compress / decompress on host bytes large enough for the
+    pipelined transfers (pinned chunks, multi-threaded lz4m_host_copy, the
+    content XXH32 hashed while staging; lz4._native _BIG / _CHUNK) at sizes
+    that are no multiple of the chunk or the copy threads: the frame decodes
+    with the compiled reference to the input, and our decoder returns it."""
+    import oracle as O
+    import lz4.frame as F
+    from lz4 import _synth
+    nblk = (size + 65535) // 65536
+    data = _synth.blocks(nblk, "silesia", seed=9).tobytes()[:size]
+    c = F.compress(data, block_size=F.BLOCKSIZE_MAX4MB, block_linked=False, content_checksum=True)
+    code, out = O.ref_decompress_frame(reference, c)
+    assert code == 0 and out == data
+    assert F.decompress(c) == data
