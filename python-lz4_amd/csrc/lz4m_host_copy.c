@@ -14,6 +14,8 @@
  * The threads are a persistent pool (created on first use, again in a forked
  * child): an 8 GiB frame is 128 calls of 64 MiB, and creating 16 threads per
  * call cost ~0.5 ms each time.  Calls from several host threads take turns.
+ * (A process that forks while one of its threads is inside a call leaves the
+ * child with that call's lock taken: fork between calls.)
  */
 #define _POSIX_C_SOURCE 200809L
 #include "../../include/lz4m.h"
