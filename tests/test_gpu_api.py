@@ -753,3 +753,41 @@ def test_frame_dropin_large_odd_sizes(gpu, reference, size):
     code, out = O.ref_decompress_frame(reference, c)
     assert code == 0 and out == data
     assert F.decompress(c) == data
+
+
+def test_exact_compress_large_batch_sampled_vs_oracle(gpu, oracle):
+    """The exact compressor at a large batch (262 144 x 64 KiB blocks, the
+    grid-stride and slot arithmetic of config-2-sized launches): 2 048 blocks
+    drawn across the batch are byte-identical to the oracle's
+    LZ4_compress_default (large-size byte identity)."""
+    import torch
+    import bench as B
+    import lz4._native as N
+    n = 262144
+    src = B.make_batch(n, 2048, "silesia", 11, gpu)
+    so, sl, slots, soff, scap, olen = B.compress_all(src, n, N.TABLE_U16_HASH4, gpu)
+    N.launch_compress(src, so, sl, slots, soff, scap, olen, n, N.TABLE_U16_HASH4, 1)
+    torch.cuda.synchronize()
+    pick = np.random.default_rng(5).choice(n, 2048, replace=False)
+    pick.sort()
+    idx = torch.from_numpy(pick).to(gpu)
+    lens = olen[idx].cpu().numpy()
+    offs = soff[idx].cpu().numpy()
+    blocks = src.view(n, -1)[idx].cpu().numpy()
+    host_slots = slots.view(-1)
+    for k, b in enumerate(pick):
+        got = host_slots[int(offs[k]): int(offs[k]) + int(lens[k])].cpu().numpy().tobytes()
+        assert got == oracle.compress(blocks[k].tobytes()), int(b)
+
+
+def test_frame_1gib_independent_is_reference_bytes(gpu, reference):
+    """lz4.frame.compress of a 1 GiB input (4 MiB independent blocks, the exact
+    parse, content checksum: config 4's frame at 1/8 of its size) is the
+    reference LZ4F_compressFrame's output byte for byte, and decodes back."""
+    import lz4.frame as F
+    from lz4 import _synth
+    data = np.tile(_synth.blocks(1024, "silesia", seed=21), (16, 1)).tobytes()   # 1 GiB
+    ours = F.compress(data, block_size=F.BLOCKSIZE_MAX4MB, block_linked=False, content_checksum=True)
+    ref = reference.compress_frame(data, block_size_id=7, linked=False, content_checksum=True, store_size=True)
+    assert ours == ref
+    assert F.decompress(ours) == data
