@@ -184,11 +184,10 @@ bool worker_enabled() {
 
 struct Workers {
     int dev = -1;
-    uint8_t* host = nullptr;       // [mailbox 0 | mailbox 1] (coherent)
+    uint8_t* host = nullptr;       // [mailbox 0 | mailbox 1] then the data regions (coherent)
     uint8_t* host_dev = nullptr;
-    uint8_t* data = nullptr;       // per kind [input kWorkIn] [record kMeta] [output kWorkOut]
+    uint8_t* data = nullptr;       // = host + kWorkMb: per kind [input kWorkIn] [record kMeta] [output kWorkOut]
     uint8_t* data_dev = nullptr;
-    bool data_own = false;         // data is its own allocation (LZ4M_WORKER_MEM=nc)
     uint8_t* dbuf = nullptr;       // device output buffers, one per kind
     hipStream_t stream[2] = {nullptr, nullptr};
     bool launched[2] = {false, false};
@@ -214,8 +213,6 @@ struct Workers {
             if (stream[k]) (void)hipStreamDestroy(stream[k]);
         if (dbuf) (void)hipFree(dbuf);
         if (host) (void)hipHostFree(host);
-        if (data && data_own) (void)hipHostFree(data);
-        data_own = false;
         host = host_dev = dbuf = data = data_dev = nullptr;
         stream[0] = stream[1] = nullptr;
     }
@@ -228,27 +225,15 @@ struct Workers {
             dev = d;
         }
         if (host) return true;
-        // the mailboxes are coherent (fine-grained): the worker polls them
-        // while it runs, with no kernel boundary to invalidate a cached copy.
-        // The request bytes: coherent too by default; LZ4M_WORKER_MEM=nc maps
-        // them non-coherent (cached in L2: the worker's system-scope acquire
-        // after each poll invalidates, its release writes back)
-        const char* me = getenv("LZ4M_WORKER_MEM");
-        const bool nc = me != nullptr && strcmp(me, "nc") == 0;
-        const unsigned cflags = hipHostMallocMapped | hipHostMallocCoherent;
-        if (hipHostMalloc(reinterpret_cast<void**>(&host), nc ? kWorkMb : kWorkMb + 2 * kRegion, cflags) != hipSuccess)
+        // coherent (fine-grained): the worker polls the mailboxes and reads
+        // each request's bytes while it runs, with no kernel boundary to
+        // invalidate a cached copy (request bytes in non-coherent, L2-cached
+        // memory measured no faster: DESIGN.md 3.3b)
+        if (hipHostMalloc(reinterpret_cast<void**>(&host), kWorkMb + 2 * kRegion,
+                          hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
             return false;
         memset(host, 0, kWorkMb);
-        if (nc) {
-            if (hipHostMalloc(reinterpret_cast<void**>(&data), 2 * kRegion, hipHostMallocMapped | hipHostMallocNonCoherent) !=
-                hipSuccess) {
-                release();
-                return false;
-            }
-            data_own = true;
-        } else {
-            data = host + kWorkMb;
-        }
+        data = host + kWorkMb;
         if (hipHostGetDevicePointer(reinterpret_cast<void**>(&host_dev), host, 0) != hipSuccess ||
             hipHostGetDevicePointer(reinterpret_cast<void**>(&data_dev), data, 0) != hipSuccess ||
             hipMalloc(reinterpret_cast<void**>(&dbuf), 2 * (kWorkOut + 256)) != hipSuccess) {
