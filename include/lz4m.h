@@ -382,6 +382,12 @@ uint32_t lz4m_xxh32_host(const void* input, size_t length, uint32_t seed);
  * lone-block kernel per call), -1 = query.  Returns the previous mode. */
 int lz4m_single_call_worker(int mode);
 
+/* count host copies dst[i] <- src[i] of n[i] bytes, spread over `threads`
+ * threads (1..16; one below 4 MiB in total) of the same pool as
+ * lz4m_host_copy: the packing and unpacking of lz4.block.compress_many /
+ * decompress_many (one H2D and one D2H staging buffer per batch). */
+void lz4m_host_copy_many(void* const* dst, const void* const* src, const size_t* n, size_t count, int threads);
+
 /* Diagnostics of the calling thread's workers (tests, tools/probe_worker.py):
  * out[0..7] = decompress / compress mailbox seq, served, quit, and the two
  * launched flags; out[8..11] = per kind the requests its last launch served

@@ -31,13 +31,22 @@ typedef struct {
     const uint8_t* src;
     size_t n;
     lz4m_xxh32_state* st; /* not NULL: hash src[0, n) into st instead of copying */
+    /* a list copy (lz4m_host_copy_many) when dsts != NULL: items [i0, i1) */
+    void* const* dsts;
+    const void* const* srcs;
+    const size_t* lens;
+    size_t i0, i1;
 } Job;
 
 static void run_job(const Job* j) {
-    if (j->st != NULL)
+    if (j->dsts != NULL) {
+        for (size_t i = j->i0; i < j->i1; ++i)
+            if (j->lens[i]) memcpy(j->dsts[i], j->srcs[i], j->lens[i]);
+    } else if (j->st != NULL) {
         lz4m_xxh32_host_update(j->st, j->src, j->n);
-    else if (j->n)
+    } else if (j->n) {
         memcpy(j->dst, j->src, j->n);
+    }
 }
 
 /* worker w (0 .. kMaxThreads - 1) runs jobs[w] of each generation it sees
@@ -104,6 +113,8 @@ static int pool(void) {
     return P.started;
 }
 
+static void run_jobs(const Job* jobs, int njobs);
+
 void lz4m_host_copy(void* dst, const void* src, size_t n, int threads, lz4m_xxh32_state* hash) {
     if (threads < 1) threads = 1;
     if (threads > kMaxThreads) threads = kMaxThreads;
@@ -119,6 +130,7 @@ void lz4m_host_copy(void* dst, const void* src, size_t n, int threads, lz4m_xxh3
         jobs[t].src = (const uint8_t*)src + lo;
         jobs[t].n = hi - lo;
         jobs[t].st = NULL;
+        jobs[t].dsts = NULL;
     }
     int njobs = threads; /* jobs[0] runs on the caller */
     if (hash) {          /* the hash reads the source concurrently with the copies */
@@ -126,8 +138,14 @@ void lz4m_host_copy(void* dst, const void* src, size_t n, int threads, lz4m_xxh3
         jobs[njobs].src = (const uint8_t*)src;
         jobs[njobs].n = n;
         jobs[njobs].st = hash;
+        jobs[njobs].dsts = NULL;
         ++njobs;
     }
+    run_jobs(jobs, njobs);
+}
+
+/* jobs[0] on the caller, the others on the pool's workers */
+static void run_jobs(const Job* jobs, int njobs) {
     if (njobs == 1) {
         run_job(&jobs[0]);
         return;
@@ -151,4 +169,32 @@ void lz4m_host_copy(void* dst, const void* src, size_t n, int threads, lz4m_xxh3
     while (P.pending > 0) pthread_cond_wait(&P.done, &P.mu);
     pthread_mutex_unlock(&P.mu);
     pthread_mutex_unlock(&P.call);
+}
+
+void lz4m_host_copy_many(void* const* dst, const void* const* src, const size_t* n, size_t count, int threads) {
+    if (count == 0) return;
+    size_t total = 0;
+    for (size_t i = 0; i < count; ++i) total += n[i];
+    if (threads < 1) threads = 1;
+    if (threads > kMaxThreads) threads = kMaxThreads;
+    if (total < ((size_t)1 << 22)) threads = 1; /* below 4 MiB a thread costs more than it copies */
+    if ((size_t)threads > count) threads = (int)count;
+    Job jobs[kMaxThreads];
+    /* contiguous item ranges of about total / threads bytes each */
+    size_t i = 0, acc = 0;
+    for (int t = 0; t < threads; ++t) {
+        const size_t goal = total / (size_t)threads * (size_t)(t + 1);
+        const size_t i0 = i;
+        while (i < count && (acc < goal || t == threads - 1)) acc += n[i++];
+        jobs[t].dst = NULL;
+        jobs[t].src = NULL;
+        jobs[t].n = 0;
+        jobs[t].st = NULL;
+        jobs[t].dsts = dst;
+        jobs[t].srcs = src;
+        jobs[t].lens = n;
+        jobs[t].i0 = i0;
+        jobs[t].i1 = i;
+    }
+    run_jobs(jobs, threads);
 }

@@ -77,6 +77,7 @@ def _declare(lib) -> None:
         "lz4m_xxh32_host_digest": ([vp], u32),
         "lz4m_xxh32_host": ([vp, C.c_size_t, u32], u32),
         "lz4m_host_copy": ([vp, vp, C.c_size_t, i32, vp], None),
+        "lz4m_host_copy_many": ([vp, vp, vp, C.c_size_t, i32], None),
         "lz4m_single_call_worker": ([i32], i32),
         "lz4m_single_call_worker_state": ([vp], i32),
     }
@@ -511,3 +512,14 @@ def to_host_bytes(t: torch.Tensor, n: int, as_bytearray: bool = False, hash_seed
             e.synchronize()
         _pinned_release(_CHUNK, bufs)
     return (out, st.digest()) if st is not None else out
+
+def host_copy_many(dsts, srcs, lens) -> None:
+    """dsts[i] <- srcs[i], lens[i] bytes each (host addresses), over the copy
+    pool (include/lz4m.h lz4m_host_copy_many)."""
+    n = len(lens)
+    if n == 0:
+        return
+    D = (C.c_void_p * n)(*dsts)
+    S = (C.c_void_p * n)(*srcs)
+    L = (C.c_size_t * n)(*lens)
+    lib().lz4m_host_copy_many(D, S, L, n, _copy_threads())

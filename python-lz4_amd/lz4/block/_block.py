@@ -258,11 +258,49 @@ def _stage_in(dev, views, offs, lens, d_off, caps, skip=None):
     hn[lay.dst_off:lay.dst_off + 8 * n].view(np.int64)[:] = d_off
     hn[lay.dst_cap:lay.dst_cap + 4 * n].view(np.int32)[:] = caps
     pos = lay.payload
-    for v in views:
-        hn[pos:pos + v.nbytes] = np.frombuffer(v, dtype=np.uint8)
-        pos += v.nbytes
+    if len(views) >= _MANY and payload >= _MANY_BYTES:   # one pooled native copy of every block
+        base = h.data_ptr()
+        dsts, srcs, ns = [], [], []
+        for v in views:
+            dsts.append(base + pos)
+            srcs.append(_addr(v))
+            ns.append(v.nbytes)
+            pos += v.nbytes
+        N.host_copy_many(dsts, srcs, ns)
+    else:
+        for v in views:
+            hn[pos:pos + v.nbytes] = np.frombuffer(v, dtype=np.uint8)
+            pos += v.nbytes
     d[:lay.h2d].copy_(h[:lay.h2d], non_blocking=True)
     return lay, h, d
+
+
+# batches of at least this many blocks and bytes pack and unpack through one
+# pooled native copy (lz4m_host_copy_many) instead of a numpy copy per block
+_MANY, _MANY_BYTES = 32, 4 << 20
+
+
+def _results_many(host, d_off, sizes, hdr_lens, as_bytearray):
+    """New bytes (or bytearrays) for blocks of sizes[i] >= 0 bytes at host
+    offset d_off[i] (None where sizes[i] < 0), prefixed with the LE32 of
+    hdr_lens[i] when hdr_lens is given; filled by one pooled copy."""
+    base = host.ctypes.data
+    res, dsts, srcs, ns = [], [], [], []
+    for i, L in enumerate(sizes):
+        if L < 0:
+            res.append(None)
+            continue
+        hdr = 4 if hdr_lens is not None else 0
+        b, addr = N._new_host_buffer(hdr + L, as_bytearray) if hdr + L else ((bytearray() if as_bytearray else b""), 0)
+        if hdr:
+            C.memmove(addr, hdr_lens[i].to_bytes(4, "little"), 4)
+        if L:
+            dsts.append(addr + hdr)
+            srcs.append(base + int(d_off[i]))
+            ns.append(L)
+        res.append(b)
+    N.host_copy_many(dsts, srcs, ns)
+    return res
 
 
 def _dev_views(lay: _Layout, d: torch.Tensor, n: int):
@@ -317,6 +355,9 @@ def compress_many(blocks, accel: int = 1, store_size: bool = True, as_bytearray:
         N.launch_compress_dict(d_src, src_off, src_len, dict_len, d_dst, dst_off, dst_cap, out_len, n, accel,
                                prefix=dict_prefix and dv.nbytes >= 8)
     olen, host = _stage_out(lay, h, d, n)
+    if n >= _MANY and sum(L for L in olen if L > 0) >= _MANY_BYTES:
+        return _results_many(host, d_off, [L if L > 0 else -1 for L in olen], lens if store_size else None,
+                             as_bytearray)
     res = []
     for i in range(n):
         L = olen[i]
@@ -386,6 +427,9 @@ def decompress_many(blocks, uncompressed_size=-1, dict=None, as_bytearray: bool 
         N.launch_decompress(d_src, src_off, src_len, d_dst, dst_off, dst_cap, status, n,
                             src_bytes=int(sum(lens)))
     st, host = _stage_out(lay, h, d, n)
+    if n >= _MANY and all(e is None for e in errors) and all(
+            r >= 0 and (r == c or us >= 0) for r, c, us in zip(st, caps, sizes)) and sum(st) >= _MANY_BYTES:
+        return _results_many(host, d_off, st, None, as_bytearray)   # every block decoded as asked
     res = []
     for i in range(n):
         if errors[i] is not None:

@@ -791,3 +791,37 @@ def test_frame_1gib_independent_is_reference_bytes(gpu, reference):
     ref = reference.compress_frame(data, block_size_id=7, linked=False, content_checksum=True, store_size=True)
     assert ours == ref
     assert F.decompress(ours) == data
+
+
+@pytest.mark.parametrize("store_size,as_bytearray", [(True, False), (False, True)])
+def test_many_calls_pooled_packing(gpu, oracle, store_size, as_bytearray):
+    """compress_many / decompress_many at batch sizes that pack and unpack
+    through one pooled native copy (lz4m_host_copy_many: >= 32 blocks and
+    >= 4 MiB): every block equals the oracle's lz4.block.compress bytes (with
+    or without the size header, bytes or bytearray), and decodes back;
+    empty and tiny blocks included."""
+    import lz4.block as LB
+    from oracle import TABLE_U32_HASH5
+    from lz4 import _synth
+    rng = np.random.default_rng(31)
+    blocks = []
+    for i in range(96):
+        if i % 17 == 0:
+            blocks.append(b"")
+        elif i % 13 == 0:
+            blocks.append(bytes(rng.integers(0, 256, int(rng.integers(1, 40)), dtype=np.uint8)))
+        elif i % 3 == 0:
+            blocks.append(rng.integers(0, 256, 65536, dtype=np.uint8).tobytes())
+        else:
+            blocks.append(_synth.blocks(1, ("silesia", "text", "records")[i % 3], seed=i).tobytes())
+    comp = LB.compress_many(blocks, store_size=store_size, as_bytearray=as_bytearray)
+    for b, c in zip(blocks, comp):
+        want = oracle.compress(b, variant=TABLE_U32_HASH5)
+        if store_size:
+            want = len(b).to_bytes(4, "little") + want
+        assert isinstance(c, bytearray if as_bytearray else bytes)
+        assert bytes(c) == want
+    sizes = -1 if store_size else [len(b) for b in blocks]
+    back = LB.decompress_many(comp, uncompressed_size=sizes, as_bytearray=as_bytearray)
+    assert [bytes(x) for x in back] == blocks
+    assert all(isinstance(x, bytearray if as_bytearray else bytes) for x in back)
