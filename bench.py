@@ -308,19 +308,29 @@ def config1(n_blocks: int, dev) -> dict:
     back = [LB.decompress(c) for c in comp]
     t2 = time.perf_counter()
     assert back == blocks, "config 1 round trip failed"
-    t3 = time.perf_counter()
-    cm = LB.compress_many(blocks)
-    t4 = time.perf_counter()
-    bm = LB.decompress_many(cm)
-    t5 = time.perf_counter()
-    assert bm == blocks and cm == comp, "config 1 batched round trip failed"
+    # batched: one untimed call of each (the first grows the pinned and
+    # device staging buffers to the batch), then the median of three
+    LB.decompress_many(LB.compress_many(blocks))
+    tc, td = [], []
+    for _ in range(3):
+        ta = time.perf_counter()
+        cm = LB.compress_many(blocks)
+        tb = time.perf_counter()
+        bm = LB.decompress_many(cm)
+        tc.append(tb - ta)
+        td.append(time.perf_counter() - tb)
+        assert bm == blocks and cm == comp, "config 1 batched round trip failed"
+        del cm, bm
+    t3, t4 = 0.0, sorted(tc)[1]
+    t5 = t4 + sorted(td)[1]
     res = {"blocks": n_blocks, "data": "random.Random(12345).randbytes(65536) per block",
            "per_call_compress_us": round((t1 - t0) / n_blocks * 1e6, 1),
            "per_call_decompress_us": round((t2 - t1) / n_blocks * 1e6, 1),
            "per_call_roundtrip_gib_s": round(tot / (t2 - t0) / GIB, 3),
            "batched_compress_gib_s": round(tot / (t4 - t3) / GIB, 3),
            "batched_decompress_gib_s": round(tot / (t5 - t4) / GIB, 3),
-           "batched_roundtrip_gib_s": round(tot / (t5 - t3) / GIB, 3)}
+           "batched_roundtrip_gib_s": round(tot / (t5 - t3) / GIB, 3),
+           "batched_note": "compress_many / decompress_many of the whole list, median of 3 after one untimed call"}
     # reference lz4libs on the host cores (LZ4_compress_default is byte-identical
     # to lz4.block.compress on random data)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
