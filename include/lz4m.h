@@ -377,7 +377,9 @@ uint32_t lz4m_xxh32_host(const void* input, size_t length, uint32_t seed);
  * on blocks up to 64 KiB) are served by a persistent one-workgroup kernel per
  * host thread and kind that polls a mailbox in mapped pinned memory, so a
  * call while others keep coming pays no kernel launch; it exits after 2 ms
- * without a call and is started again by the next one.  mode 1 = on (the
+ * without a call or 5 ms after it started (whatever the call rate: work on a
+ * stream that shares its hardware queue waits at most that long) and is
+ * started again by the next call.  mode 1 = on (the
  * default; env LZ4M_WORKER=0 turns it off), 0 = off (one launch of the
  * lone-block kernel per call), -1 = query.  Returns the previous mode. */
 int lz4m_single_call_worker(int mode);
@@ -391,10 +393,12 @@ void lz4m_host_copy_many(void* const* dst, const void* const* src, const size_t*
 /* Diagnostics of the calling thread's workers (tests, tools/probe_worker.py):
  * out[0..7] = decompress / compress mailbox seq, served, quit, and the two
  * launched flags; out[8..11] = per kind the requests its last launch served
- * and how that launch ended (1 idle, 2 quit); out[12..15] = per kind the
- * poll's real-time stamps (LZ4M_WORKER_TS builds).  Returns the number of
- * requests a worker neither served nor gave up within 1 s (each one turned
- * the worker off).  Host memory only: no HIP call. */
+ * and how that launch ended (1 idle, 2 quit, 3 lifetime); out[12..15] = per
+ * kind the poll's real-time stamps (LZ4M_WORKER_TS builds).  Returns the
+ * number of calls (process-wide) the worker path handed to the launch path:
+ * a worker that neither served nor exited within 1 s, a stream error, more
+ * than three restarts in one call, a failed start, a lone-block staging wait
+ * that gave up.  Host memory only: no HIP call. */
 int lz4m_single_call_worker_state(uint32_t out[16]);
 
 /* Host memcpy of n bytes split over `threads` threads (1..16; one below

@@ -329,13 +329,25 @@ __device__ __forceinline__ uint32_t lw_before(const uint8_t* w, int32_t p) {   /
 // chunk c is in LDS.  lw_need(x) waits until bytes [0, x) are; `have` (wave
 // uniform) is what the parse already knows to be staged.
 constexpr int32_t kStageChunk = 4096;
+// stage[kStageFail] != 0: a wait gave up (the staged bytes never came); the
+// parse then runs on to its end without waiting and the lone-block kernel
+// reports kSoloStageFail instead of the bytes it made (no
+// silently wrong block)
+constexpr int32_t kStageFail = 17;
+constexpr int32_t kSoloStageFail = -2;   // internal result: redo the call another way (lz4m_host.hip)
 typedef __attribute__((address_space(3))) volatile int32_t lds_vi32;
 __device__ __forceinline__ void lw_need(const int32_t* stage, int32_t& have, int32_t x) {
     if (stage == nullptr) return;
     while (have < x) {
         const lds_vi32* f = (const lds_vi32*)stage;
         const int32_t c = have / kStageChunk;
-        for (uint32_t spins = 0; f[c] == 0 && spins < (1u << 22); ++spins) __builtin_amdgcn_s_sleep(1);
+        uint32_t spins = 0;
+        for (; f[c] == 0 && spins < (1u << 22); ++spins) __builtin_amdgcn_s_sleep(1);
+        if (spins == (1u << 22)) {   // (~0.1 s): give up, flag it, wait no more
+            *(lds_vi32*)(const_cast<int32_t*>(stage) + kStageFail) = 1;
+            have = INT32_MAX;
+            return;
+        }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         have += kStageChunk;
     }
@@ -801,7 +813,8 @@ __device__ __forceinline__ void compress_solo_body(const uint8_t* __restrict__ s
     // LDS; wave 0 zeroes the table and parses meanwhile, waiting for a chunk
     // only when it reaches it (lw_need): the PCIe staging overlaps the parse.
     constexpr int kStages = (kSoloBuf + kStageChunk - 1) / kStageChunk;
-    if (t < kStages) stage[t] = 0;
+    static_assert(kStages == kStageFail, "the failure flag follows the chunk flags");
+    if (t <= kStages) stage[t] = 0;   // the chunk flags and stage[kStageFail]
     if (t == 0) last_lit[0] = -1;
     __syncthreads();
     const uint32_t wv = t >> 6, ln = t & 63;
@@ -837,8 +850,11 @@ __device__ __forceinline__ void compress_solo_body(const uint8_t* __restrict__ s
     LZ4M_WTS(ts, 2);
     // the compressed bytes from LDS to the caller's mapped host buffer (or to
     // dst), all four waves: LDS reads and stores only, nothing waits on a
-    // store.  The last literals come straight from the staged block.
-    const int32_t r = solo_r;
+    // store.  The last literals come straight from the staged block.  A
+    // staging wait that gave up: no bytes, kSoloStageFail.
+    const bool sfail = *(const lds_vi32*)(stage + kStageFail) != 0;
+    if (sfail && t == 0) *out_len = kSoloStageFail;
+    const int32_t r = sfail ? 0 : solo_r;
     uint8_t* out = h_out != nullptr ? h_out : dst;
     const int32_t split = r > 0 && last_lit[0] >= 0 ? last_lit[0] : r;   // [0, split) in obuf
     for (int32_t p = 16 * (int32_t)t; p < split; p += kStep) {
@@ -1196,7 +1212,7 @@ template <int V, bool ACC1>
 __global__ __launch_bounds__(256) void compress_solo_kernel(const uint8_t* __restrict__ src, int32_t len,
                                                             uint8_t* dst, int32_t cap, int32_t* __restrict__ out_len,
                                                             int accel, uint8_t* h_out, int32_t* h_done) {
-    __shared__ int32_t solo_r, last_lit[2], stage[(kSoloBuf + kStageChunk - 1) / kStageChunk];
+    __shared__ int32_t solo_r, last_lit[2], stage[kStageFail + 1];
     __shared__ __attribute__((aligned(16))) uint8_t blk[kSoloBuf];
     __shared__ __attribute__((aligned(16))) uint8_t obuf[kSoloOut];
     __shared__ __attribute__((aligned(16))) uint16_t tab[8192];
@@ -1208,16 +1224,18 @@ __global__ __launch_bounds__(256) void compress_solo_kernel(const uint8_t* __res
 // The single-call compress worker (lz4m_worker.h): one persistent workgroup
 // serving lone-block compress requests from its mailbox with the solo body;
 // the LDS buffers are declared once here and shared by every table variant.
-__global__ __launch_bounds__(256) void compress_worker(Mailbox* mb, uint8_t* hd, uint8_t* dbuf, uint64_t idle) {
+__global__ __launch_bounds__(256) void compress_worker(Mailbox* mb, uint8_t* hd, uint8_t* dbuf, uint64_t idle,
+                                                      uint64_t life) {
     __shared__ uint32_t cmd[8];
-    __shared__ int32_t solo_r, last_lit[2], stage[(kSoloBuf + kStageChunk - 1) / kStageChunk];
+    __shared__ int32_t solo_r, last_lit[2], stage[kStageFail + 1];
     __shared__ __attribute__((aligned(16))) uint8_t blk[kSoloBuf];
     __shared__ __attribute__((aligned(16))) uint8_t obuf[kSoloOut];
     __shared__ __attribute__((aligned(16))) uint16_t tab[8192];
     RING_DECL
-    uint32_t last = worker_init(mb, cmd);
+    uint64_t birth = 0;
+    uint32_t last = worker_init(mb, cmd, birth);
     for (;;) {
-        if (worker_next(mb, last, idle, cmd) == 0) break;
+        if (worker_next(mb, last, idle, birth, life, cmd) == 0) break;
         const int32_t rec_off = (int32_t)cmd[1], len = (int32_t)cmd[2], cap = (int32_t)cmd[3];
         const int table = (int)cmd[4];
         int accel = (int)cmd[5];
@@ -1248,8 +1266,8 @@ __global__ __launch_bounds__(256) void compress_worker(Mailbox* mb, uint8_t* hd,
 using namespace lz4m;
 
 extern "C" int lz4m_compress_worker_launch(Mailbox* mb, uint8_t* hd, uint8_t* dbuf, uint64_t idle_ticks,
-                                           hipStream_t stream) {
-    hipLaunchKernelGGL(compress_worker, dim3(1), dim3(256), 0, stream, mb, hd, dbuf, idle_ticks);
+                                           uint64_t life_ticks, hipStream_t stream) {
+    hipLaunchKernelGGL(compress_worker, dim3(1), dim3(256), 0, stream, mb, hd, dbuf, idle_ticks, life_ticks);
     return (int)hipGetLastError();
 }
 

@@ -1237,13 +1237,15 @@ __global__ __launch_bounds__(256, 4) void hist_decompress_kernel(const uint8_t* 
 // the lone-block requests of one host thread from its mailbox with the
 // SOLO body above (input and record read from mapped pinned memory, output
 // written back into it, done flag released), until told to quit or idle.
-__global__ __launch_bounds__(256) void decompress_worker(Mailbox* mb, uint8_t* hd, uint8_t* dbuf, uint64_t idle) {
+__global__ __launch_bounds__(256) void decompress_worker(Mailbox* mb, uint8_t* hd, uint8_t* dbuf, uint64_t idle,
+                                                        uint64_t life) {
     __shared__ uint32_t cmd[8];
     __shared__ int64_t zero_off;   // the record's offsets and sizes, read by the body from LDS, not over PCIe
-    uint32_t last = worker_init(mb, cmd);
+    uint64_t birth = 0;
+    uint32_t last = worker_init(mb, cmd, birth);
     if (threadIdx.x == 0) zero_off = 0;
     for (;;) {
-        if (worker_next(mb, last, idle, cmd) == 0) break;
+        if (worker_next(mb, last, idle, birth, life, cmd) == 0) break;
         const int32_t rec_off = (int32_t)cmd[1];
         CallMeta* rec = reinterpret_cast<CallMeta*>(hd + rec_off);
         const int32_t* len_cap = reinterpret_cast<const int32_t*>(cmd + 2);   // cmd[2] = src_len, cmd[3] = dst_cap
@@ -1430,10 +1432,10 @@ extern "C" int lz4m_decompress_solo(const uint8_t* d_src, const int64_t* d_src_o
 }
 
 extern "C" int lz4m_worker_launch(int kind, Mailbox* mb, uint8_t* hd, uint8_t* dbuf, uint64_t idle_ticks,
-                                  hipStream_t stream) {
-    if (kind == 1) return lz4m_compress_worker_launch(mb, hd, dbuf, idle_ticks, stream);
+                                  uint64_t life_ticks, hipStream_t stream) {
+    if (kind == 1) return lz4m_compress_worker_launch(mb, hd, dbuf, idle_ticks, life_ticks, stream);
     if (kind != 0) return LZ4M_EINVAL;
-    hipLaunchKernelGGL(decompress_worker, dim3(1), dim3(256), 0, stream, mb, hd, dbuf, idle_ticks);
+    hipLaunchKernelGGL(decompress_worker, dim3(1), dim3(256), 0, stream, mb, hd, dbuf, idle_ticks, life_ticks);
     return (int)hipGetLastError();
 }
 

@@ -161,17 +161,29 @@ int32_t one_block_mapped(const char* src, int32_t len, char* dst, int32_t cap, i
 // A lone call served by a persistent one-workgroup kernel that polls a
 // mailbox in mapped pinned memory (lz4m_worker.h): while calls keep coming,
 // none of them pays a kernel launch.  One worker per kind (decompress /
-// compress) and host thread; it exits by itself after kIdle of no requests
-// (so a stream it shares a hardware queue with waits at most that long), on
-// the host's quit, or when the thread ends.  A call whose worker has exited
-// starts it again; calls outside its buffers take the launch-per-call path.
+// compress) and host thread; it exits by itself after kIdle of no requests,
+// after kLife in total (so a stream it shares a hardware queue with waits at
+// most that long, whatever the call rate), on the host's quit, or when the
+// thread ends.  A call whose worker has exited starts it again; calls outside
+// its buffers take the launch-per-call path.
 constexpr size_t kWorkIn = 66 * 1024;         // input region: the lone-block kernels' ranges
 constexpr size_t kWorkOut = 1 << 20;          // output region: capacities up to 1 MiB
 constexpr size_t kWorkMb = 128;               // two mailboxes
 constexpr uint64_t kIdle = 200000;            // 2 ms of the 100 MHz real-time clock
+constexpr uint64_t kLife = 500000;            // 5 ms: a launch's whole lifetime
+constexpr int32_t kSoloStageFail = -2;        // lone-block compress: a staging wait gave up (lz4m_compress.hip)
 
 std::atomic<int> g_worker_mode{-1};           // -1: from LZ4M_WORKER at first use
-std::atomic<int> g_worker_failures{0};        // requests a worker neither served nor gave up within 1 s
+// every call the worker path took and then handed to the launch path: a
+// worker that neither served nor exited within 1 s, a stream error, more than
+// three restarts in one call, a failed (re)start, a lone-block staging wait
+// that gave up.  Each one but the last also turns the worker path off for the
+// process.  Tests assert it stays 0 (tests/conftest.py).
+std::atomic<int> g_worker_failures{0};
+void worker_failed(bool turn_off) {
+    g_worker_failures.fetch_add(1, std::memory_order_relaxed);
+    if (turn_off) g_worker_mode.store(0, std::memory_order_relaxed);
+}
 bool worker_enabled() {
     int m = g_worker_mode.load(std::memory_order_relaxed);
     if (m < 0) {
@@ -197,18 +209,41 @@ struct Workers {
     size_t region(int k) const { return (size_t)k * kRegion; }
     uint8_t* base(int k) { return data + region(k); }
     bool idle(int k) { return hipStreamQuery(stream[k]) == hipSuccess; }
-    void stop(int k) {
-        if (!launched[k]) return;
+    // Tell worker k to quit and wait (<= 2 s) until its stream is idle.
+    // Returns false if it is still queued or running: its mailbox keeps
+    // quit = 1 and the caller abandons this whole set (abandon()), so a late
+    // worker exits without touching a live request.
+    bool stop(int k) {
+        if (!launched[k]) return true;
         __atomic_store_n(&mb(k)->quit, 1u, __ATOMIC_RELEASE);
         const auto t0 = std::chrono::steady_clock::now();
-        while (hipStreamQuery(stream[k]) == hipErrorNotReady &&
+        hipError_t q;
+        while ((q = hipStreamQuery(stream[k])) == hipErrorNotReady &&
                std::chrono::steady_clock::now() - t0 < std::chrono::seconds(2))
             __builtin_ia32_pause();
+        if (q == hipErrorNotReady) return false;
         launched[k] = false;
         __atomic_store_n(&mb(k)->quit, 0u, __ATOMIC_RELEASE);
+        return true;
+    }
+    // Drop this set of mailboxes, staging regions, device buffers and streams
+    // without freeing them (a worker that did not stop may still read and
+    // write them); the next get() allocates a fresh set.
+    void abandon() {
+        host = host_dev = dbuf = data = data_dev = nullptr;
+        stream[0] = stream[1] = nullptr;
+        launched[0] = launched[1] = false;
+        seq[0] = seq[1] = 0;
+        dev = -1;
+    }
+    // stop both workers; abandon the set if either did not stop
+    bool stop_all() {
+        const bool a = stop(0), b = stop(1);
+        if (!(a && b)) abandon();
+        return a && b;
     }
     void release() {
-        for (int k = 0; k < 2; ++k) stop(k);
+        if (!stop_all()) return;   // abandoned: nothing of it may be freed
         for (int k = 0; k < 2; ++k)
             if (stream[k]) (void)hipStreamDestroy(stream[k]);
         if (dbuf) (void)hipFree(dbuf);
@@ -252,7 +287,7 @@ struct Workers {
         if (launched[k]) return true;
         __atomic_store_n(&mb(k)->quit, 0u, __ATOMIC_RELEASE);
         if (lz4m_worker_launch(k, reinterpret_cast<lz4m::Mailbox*>(host_dev + 64 * k), data_dev + region(k),
-                               dbuf + (size_t)k * (kWorkOut + 256), kIdle, stream[k]) != 0)
+                               dbuf + (size_t)k * (kWorkOut + 256), kIdle, kLife, stream[k]) != 0)
             return false;
         launched[k] = true;
         return true;
@@ -269,7 +304,10 @@ bool one_block_worker(int kind, const char* src, int32_t len, char* dst, int32_t
     const int32_t out_cap = kind == 1 ? lz4m_compress_bound(len) : cap;
     if (in > kWorkIn || out_cap > (int32_t)kWorkOut || len < 0) return false;
     Workers& W = t_workers;
-    if (!W.get()) return false;
+    if (!W.get()) {
+        worker_failed(true);
+        return false;
+    }
     uint8_t* h = W.base(kind);
     if (len) memcpy(h, src, (size_t)len);
     CMeta m{};
@@ -285,42 +323,53 @@ bool one_block_worker(int kind, const char* src, int32_t len, char* dst, int32_t
     M->dst_cap = cap;
     M->table = table;
     M->accel = accel;
-    if (!W.start(kind)) return false;
+    if (!W.start(kind)) {
+        worker_failed(true);
+        return false;
+    }
     if (++W.seq[kind] == 0) W.seq[kind] = 1;
     __atomic_store_n(&M->seq, W.seq[kind], __ATOMIC_RELEASE);
     CMeta* hm = reinterpret_cast<CMeta*>(h + in);
     int restarts = 0;
     const auto t0 = std::chrono::steady_clock::now();
-    // every 256 polls: has the worker exited without serving (it went idle
-    // as the request arrived)?  Then start it again; it serves the request.
-    // A worker that neither serves nor exits within a second is stopped and
-    // the worker path is turned off for the process (the launch path then
-    // serves every call): a call never waits on it without bound.
+    // every 256 polls: has the worker exited without serving (it went idle or
+    // reached its lifetime as the request arrived)?  Then start it again; it
+    // serves the request.  A worker that neither serves nor exits within a
+    // second is stopped and the worker path is turned off for the process
+    // (the launch path then serves every call): a call never waits on it
+    // without bound.  Every hand-over to the launch path is counted.
     for (uint32_t i = 1; __atomic_load_n(&hm->done, __ATOMIC_ACQUIRE) == 0; ++i) {
         if ((i & 255) == 0) {
             const hipError_t q = hipStreamQuery(W.stream[kind]);
             if (__atomic_load_n(&hm->done, __ATOMIC_ACQUIRE) != 0) break;
-            if (q != hipSuccess && q != hipErrorNotReady) {
-                g_worker_mode.store(0, std::memory_order_relaxed);
+            if (q != hipSuccess && q != hipErrorNotReady) {   // the stream failed: this set is unusable
+                worker_failed(true);
+                W.abandon();
                 return false;
             }
             if (q == hipSuccess) {
                 if (++restarts > 3) {
-                    g_worker_mode.store(0, std::memory_order_relaxed);
+                    worker_failed(true);
                     return false;
                 }
                 W.launched[kind] = false;
-                if (!W.start(kind)) return false;
+                if (!W.start(kind)) {
+                    worker_failed(true);
+                    return false;
+                }
             } else if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(1)) {
-                g_worker_failures.fetch_add(1, std::memory_order_relaxed);
-                g_worker_mode.store(0, std::memory_order_relaxed);
-                W.stop(kind);
+                worker_failed(true);
+                W.stop_all();
                 return false;
             }
         }
         __builtin_ia32_pause();
     }
     memcpy(&m, h + in, sizeof m);
+    if (kind == 1 && m.result == kSoloStageFail) {   // the block never reached LDS: redo it by launch
+        worker_failed(false);
+        return false;
+    }
     t_out = h + in + kMeta;
     if (dst && m.result > 0 && m.result <= cap) memcpy(dst, h + in + kMeta, (size_t)m.result);
     *result = m.result;
@@ -341,7 +390,8 @@ int compress_one(const char* src, char* dst, int srcSize, int dstCapacity, int t
                 return lz4m_compress_solo(hd, srcSize, d, dstCapacity, &hm->result, table, acceleration, hout,
                                           &hm->done, reinterpret_cast<lz4m_stream_t>(s));
             });
-        return r > 0 ? r : 0;
+        if (r != kSoloStageFail) return r > 0 ? r : 0;
+        worker_failed(false);   // staging gave up on the launch path too: the batched kernel below
     }
     const int32_t r = one_block(src, srcSize, dst, dstCapacity, 0, [&](uint8_t* d, CMeta* dm, hipStream_t s) {
         return lz4m_compress_batch(d, &dm->src_off, &dm->src_len, d, &dm->dst_off, &dm->dst_cap, &dm->result, 1,
@@ -433,10 +483,7 @@ extern "C" int lz4m_single_call_worker(int mode) {
     const int prev = worker_enabled() ? 1 : 0;
     if (mode == 0 || mode == 1) {
         g_worker_mode.store(mode, std::memory_order_relaxed);
-        if (mode == 0) {   // this thread's workers stop now (other threads' go idle by themselves)
-            t_workers.stop(0);
-            t_workers.stop(1);
-        }
+        if (mode == 0) t_workers.stop_all();   // this thread's workers stop now (other threads' go idle by themselves)
     }
     return prev;
 }

@@ -630,6 +630,9 @@ constexpr int32_t kRowsH = LZ4M_ROWS_H;
 #ifndef LZ4M_ROWS_PASS1
 #define LZ4M_ROWS_PASS1 0     // A/B: a first readiness pass without the row scans (sources before the round)
 #endif
+#ifndef LZ4M_ROWS_XP
+#define LZ4M_ROWS_XP 0      // timing probes (bits 2, 4, 8 give WRONG output): 1 sync-path drain, 2 no HBM loads in passes, 4 no late loads, 8 no far prefetch
+#endif
 #ifndef LZ4M_ROWS_COUNTED
 #define LZ4M_ROWS_COUNTED 0   // A/B: a fixed number of memory operations per round on the common path (measured -1 %)
 #endif
@@ -750,7 +753,8 @@ __device__ __forceinline__ void parse_round(PSeq& P, int32_t jj, int32_t r, int3
     const bool late = far & (s0 + 32 > F);
     const bool pf = far & !late;
     // unconditional requests (lanes without a far source read the block start)
-    P.pre0 = ld16(d + (pf ? s0 : 0));
+    if (LZ4M_ROWS_XP & 8) P.pre0 = u32x4{(uint32_t)s0, 0, 0, 0};
+    else P.pre0 = ld16(d + (pf ? s0 : 0));
     const uint32_t sh = (uint32_t)lp;
     XS[0] = u32x4{__builtin_amdgcn_alignbyte(wa.y, wa.x, sh), __builtin_amdgcn_alignbyte(wa.z, wa.y, sh),
                  __builtin_amdgcn_alignbyte(wa.w, wa.z, sh), __builtin_amdgcn_alignbyte(wb.x, wa.w, sh)};
@@ -905,6 +909,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LZ4M_ROWS_WA
             load_in(s, P.ipn + row_incl_sum(dn) - dn, iend, na, nb);
             dnn = load_len(dl, k0 + 32 + jj, nseq);
             sync = false;
+            if (LZ4M_ROWS_XP & 1) wait_vm0();
 #if LZ4M_ROWS_COUNTED
             wait_vm0();   // (rare: block starts, short rounds) the common path's waits stay counted
 #endif
@@ -1011,7 +1016,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LZ4M_ROWS_WA
         // the round writes into its source [s0, se)
         const bool far = (P.fl & kFlFar) != 0, late = (P.fl & kFlLate) != 0;
         u32x4 g0 = P.pre0;
-            if (__any(late)) {   // a source flushed only by the previous round (rare): load it now
+            if (!(LZ4M_ROWS_XP & 4) && __any(late)) {   // a source flushed only by the previous round (rare): load it now
             const u32x4 lv = ld16(d + (late ? s0 : 0));
             g0 = late ? lv : g0;
 #if LZ4M_ROWS_COUNTED
@@ -1035,7 +1040,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LZ4M_ROWS_WA
                     if (!per) {
                         const int32_t sp = s0 + i;
                         // sp < base: flushed (F >= base + kRowsKeep - 16)
-                        v = sp >= base ? lds_ld16u(HB + (sp - base)) : ld16(d + sp);
+                        if (LZ4M_ROWS_XP & 2) v = lds_ld16u(HB + (sp >= base ? sp - base : 0));
+                        else v = sp >= base ? lds_ld16u(HB + (sp - base)) : ld16(d + sp);
                     }
                     LDS_PUT(HB + (m - base + i), v, ml - i);
                 }

@@ -152,21 +152,30 @@ __global__ __launch_bounds__(256) void frame_emit_kernel(const uint8_t* __restri
     }
 }
 
-// lane per block: block checksum = XXH32 of the payload (lz4frame.c:844-847),
-// read back from the frame buffer after frame_emit_kernel.
-__global__ __launch_bounds__(256) void frame_block_crc_kernel(uint8_t* __restrict__ frame,
-                                                              const int64_t* __restrict__ frame_off,
-                                                              const int32_t* __restrict__ raw_len,
-                                                              const int32_t* __restrict__ cmp_len, int64_t n) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const int64_t L = stored_raw(raw_len[i], cmp_len[i]) ? raw_len[i] : cmp_len[i];
-    uint8_t* d = frame + frame_off[i] + 4;
-    const uint32_t c = xxh32_lane(d, L, 0);
-    d[L] = (uint8_t)c;
-    d[L + 1] = (uint8_t)(c >> 8);
-    d[L + 2] = (uint8_t)(c >> 16);
-    d[L + 3] = (uint8_t)(c >> 24);
+// quad per block (xxh32_quad_acc): block checksum = XXH32 of the payload
+// (lz4frame.c:844-847), read back from the frame buffer after
+// frame_emit_kernel; 16 blocks per 64-lane workgroup.
+__global__ __launch_bounds__(64) void frame_block_crc_kernel(uint8_t* __restrict__ frame,
+                                                             const int64_t* __restrict__ frame_off,
+                                                             const int32_t* __restrict__ raw_len,
+                                                             const int32_t* __restrict__ cmp_len, int64_t n) {
+    const uint32_t l = threadIdx.x, a = l & 3u;
+    const int64_t i = (int64_t)blockIdx.x * 16 + (l >> 2);
+    const bool live = i < n;
+    const int64_t L = live ? (stored_raw(raw_len[i], cmp_len[i]) ? raw_len[i] : cmp_len[i]) : 0;
+    uint8_t* d = frame + (live ? frame_off[i] + 4 : 0);
+    const uint32_t n16 = (uint32_t)(L >> 4);
+    const uint32_t steps = wave_max_u32(n16);
+    const uint64_t has = __ballot(n16 > 0);
+    const uint8_t* dv = n16 > 0 ? d : (has ? (const uint8_t*)readlane64((int64_t)(uintptr_t)d, __builtin_ctzll(has)) : d);
+    const uint32_t v = xxh32_quad_acc(dv, n16, steps, 0, a);
+    const uint32_t c = xxh32_quad_finish(v, d, L, 0);
+    if (live && a == 0) {
+        d[L] = (uint8_t)c;
+        d[L + 1] = (uint8_t)(c >> 8);
+        d[L + 2] = (uint8_t)(c >> 16);
+        d[L + 3] = (uint8_t)(c >> 24);
+    }
 }
 
 
@@ -278,7 +287,7 @@ extern "C" int lz4m_frame_emit(const uint8_t* d_raw, const int64_t* d_raw_off, c
     hipLaunchKernelGGL(frame_emit_kernel, dim3((uint32_t)((n + 3) / 4)), dim3(256), 0, s, d_raw, d_raw_off,
                        d_raw_len, d_cmp, d_cmp_off, d_cmp_len, d_frame, d_frame_off, n);
     if (block_checksum)
-        hipLaunchKernelGGL(frame_block_crc_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, d_frame,
+        hipLaunchKernelGGL(frame_block_crc_kernel, dim3((uint32_t)((n + 15) / 16)), dim3(64), 0, s, d_frame,
                            d_frame_off, d_raw_len, d_cmp_len, n);
     return (int)hipGetLastError();
 }

@@ -23,8 +23,10 @@ static_assert(sizeof(CallMeta) <= kCallMeta, "record size");
 // A worker's mailbox (mapped pinned host memory, one per worker kind and host
 // thread).  The host writes the request fields, then `seq` with a release; the
 // worker's lane 0 polls `seq` (system-scope acquire), serves the request with
-// the lone-block kernel's own body, then stores `served` before it polls again.  It exits on `quit`
-// or after `idle` ticks of the 100 MHz real-time clock without a request.
+// the lone-block kernel's own body, then stores `served` before it polls again.  It exits on `quit`,
+// after `idle` ticks of the 100 MHz real-time clock without a request, or, between requests, once
+// it has run `life` ticks: a stream that shares its hardware queue waits at most that long even
+// while calls keep coming (the host starts it again on the next call).
 struct Mailbox {
     uint32_t seq;       // host: request number (never 0)
     uint32_t quit;      // host: 1 = exit now
@@ -34,7 +36,7 @@ struct Mailbox {
     int32_t src_len;    // request: input bytes (at offset 0)
     int32_t dst_cap;    // request: output capacity
     int32_t table;      // request (compress): LZ4M_TABLE_*
-    uint32_t pad[8];    // worker diagnostics: [0] requests served by this launch, [1] exit reason (1 idle, 2 quit)
+    uint32_t pad[8];    // worker diagnostics: [0] requests served by this launch, [1] exit reason (1 idle, 2 quit, 3 lifetime)
 };
 static_assert(sizeof(Mailbox) == 64 && offsetof(Mailbox, rec_off) == 16, "mailbox layout");
 
@@ -58,7 +60,8 @@ static_assert(sizeof(Mailbox) == 64 && offsetof(Mailbox, rec_off) == 16, "mailbo
 // 0 = exit.  Fields of the request land in cmd[1..5]; cmd[6] counts the
 // requests served.  `last` is the request just served (0: none yet): once every
 // thread is past it, lane 0 publishes it as `served` before polling again.
-__device__ __forceinline__ uint32_t worker_next(Mailbox* mb, uint32_t& last, uint64_t idle, uint32_t* cmd) {
+__device__ __forceinline__ uint32_t worker_next(Mailbox* mb, uint32_t& last, uint64_t idle, uint64_t birth, uint64_t life,
+                                                uint32_t* cmd) {
     __syncthreads();   // every thread is past the previous request and its reads of cmd
     if (threadIdx.x == 0) {
         if (last != 0) {
@@ -72,6 +75,12 @@ __device__ __forceinline__ uint32_t worker_next(Mailbox* mb, uint32_t& last, uin
             seq = __hip_atomic_load(&mb->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
             if (__hip_atomic_load(&mb->quit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) {
                 why = 2;
+                break;
+            }
+            // lifetime over: exit even with a request pending (the host sees the
+            // stream idle and starts a new launch, which serves it)
+            if (__builtin_amdgcn_s_memrealtime() - birth > life) {
+                why = 3;
                 break;
             }
             if (seq != last) {
@@ -106,8 +115,10 @@ __device__ __forceinline__ uint32_t worker_next(Mailbox* mb, uint32_t& last, uin
     return last;
 }
 
-// a worker's first act: the served count starts at 0, `last` at the mailbox's served
-__device__ __forceinline__ uint32_t worker_init(Mailbox* mb, uint32_t* cmd) {
+// a worker's first act: the served count starts at 0, `last` at the mailbox's
+// served, `birth` (thread 0's) at the real-time clock
+__device__ __forceinline__ uint32_t worker_init(Mailbox* mb, uint32_t* cmd, uint64_t& birth) {
+    birth = __builtin_amdgcn_s_memrealtime();
     if (threadIdx.x == 0) {
         cmd[6] = mb->served != 0 ? ~0u : 0u;   // the first publication re-stores the served number
         __hip_atomic_store(&mb->pad[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -120,9 +131,10 @@ __device__ __forceinline__ uint32_t worker_init(Mailbox* mb, uint32_t* cmd) {
 extern "C" {
 // launch the persistent worker of `kind` (0 = decompress, 1 = compress) on
 // `stream`: mailbox mb, staging buffer hd (device views of mapped pinned
-// memory), device output buffer dbuf
+// memory), device output buffer dbuf; idle / lifetime limits in ticks of the
+// 100 MHz real-time clock
 int lz4m_worker_launch(int kind, lz4m::Mailbox* mb, uint8_t* hd, uint8_t* dbuf, uint64_t idle_ticks,
-                       hipStream_t stream);
+                       uint64_t life_ticks, hipStream_t stream);
 int lz4m_compress_worker_launch(lz4m::Mailbox* mb, uint8_t* hd, uint8_t* dbuf, uint64_t idle_ticks,
-                                hipStream_t stream);
+                                uint64_t life_ticks, hipStream_t stream);
 }

@@ -4,8 +4,8 @@
 // digest it equals over a whole buffer (xxhash.c:437-554; total length taken
 // mod 2^32, xxhash.c:464).
 //
-// Batch kernel: one lane per item (block checksums, lz4frame.c:846/1819);
-// each lane streams its item in 16-byte stripes.
+// Batch kernel: one quad (4 lanes, one per accumulator) per item (block
+// checksums, lz4frame.c:846/1819; config 5's root consumer).
 // Long kernel: one wavefront for a single buffer (content checksum,
 // lz4frame.c:1042/1171).  XXH32's four accumulators are serial recurrences
 // with no associative combine: one wave per
@@ -16,12 +16,27 @@
 
 namespace lz4m {
 
-__global__ __launch_bounds__(256) void xxh32_batch_kernel(const uint8_t* __restrict__ src,
-                                                          const int64_t* __restrict__ off,
-                                                          const int64_t* __restrict__ len, uint32_t seed,
-                                                          uint32_t* __restrict__ out, int64_t n) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) out[i] = xxh32_lane(src + off[i], len[i], seed);
+// One quad per item (xxh32_quad_acc): 16 items per 64-lane workgroup, so a
+// batch of n items occupies n / 16 waves of the chip (config 5's 4 096-item
+// pages: 256 waves, one per CU), each lane streaming its accumulator's words
+// with 2 x kXQ loads in flight.
+__global__ __launch_bounds__(64) void xxh32_batch_kernel(const uint8_t* __restrict__ src,
+                                                         const int64_t* __restrict__ off,
+                                                         const int64_t* __restrict__ len, uint32_t seed,
+                                                         uint32_t* __restrict__ out, int64_t n) {
+    const uint32_t l = threadIdx.x, a = l & 3u;
+    const int64_t i = (int64_t)blockIdx.x * 16 + (l >> 2);
+    const bool live = i < n;
+    const int64_t L = live ? len[i] : 0;
+    const uint8_t* p = src + (live ? off[i] : 0);
+    const uint32_t n16 = (uint32_t)(L >> 4);
+    const uint32_t steps = wave_max_u32(n16);
+    // lanes with no full stripe point at an item that has one (never read past it)
+    const uint64_t has = __ballot(n16 > 0);
+    const uint8_t* pv = n16 > 0 ? p : (has ? (const uint8_t*)readlane64((int64_t)(uintptr_t)p, __builtin_ctzll(has)) : p);
+    const uint32_t v = xxh32_quad_acc(pv, n16, steps, seed, a);
+    const uint32_t h = xxh32_quad_finish(v, p, L, seed);
+    if (live && a == 0) out[i] = h;
 }
 
 // Single-buffer XXH32: XXH32's four accumulators are independent serial
@@ -92,7 +107,7 @@ extern "C" int lz4m_xxh32_batch(const uint8_t* d_src, const int64_t* d_off, cons
                                 uint32_t* d_out, int64_t n, lz4m_stream_t stream) {
     if (n < 0) return LZ4M_EINVAL;
     if (n == 0) return 0;
-    hipLaunchKernelGGL(xxh32_batch_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+    hipLaunchKernelGGL(xxh32_batch_kernel, dim3((uint32_t)((n + 15) / 16)), dim3(64), 0, (hipStream_t)stream,
                        d_src, d_off, d_len, seed, d_out, n);
     return (int)hipGetLastError();
 }

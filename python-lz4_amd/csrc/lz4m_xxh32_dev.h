@@ -74,4 +74,69 @@ __device__ uint32_t xxh32_lane(const uint8_t* p, int64_t len, uint32_t seed) {
     return xfinish(h, p + q, (int)(len - q));
 }
 
+// ---------------------------------------------------- quad-per-item XXH32
+// One QUAD (4 lanes) per item: lane a (= lane & 3) runs accumulator v[a+1]
+// of XXH32_endian_align (xxhash.c:357-368) alone -- the four accumulators
+// are independent serial recurrences, so an item's stripes split four ways
+// and no further.  Each lane reads only its own word of every 16-byte stripe
+// (a wave-instruction = one stripe of each of the wave's 16 items), and keeps
+// 2 x kXQ loads in flight (two register sets, so a set is consumed only after
+// the other was issued: a consumption never waits on the newest loads).  A
+// batch of few long items (config 5's pages: 4 096 compressed blocks of ~34
+// KiB) then has 16 384 lanes streaming, not 4 096 lanes stalled on one
+// 16-byte round trip each.  Returns the lane's accumulator after the item's
+// n16 full stripes; `steps` = the wave's largest n16 (uniform), p = the item
+// (any valid address when n16 == 0, never read then).
+constexpr int kXQ = 24;
+typedef __attribute__((address_space(1))) const uint32_t gu32;
+__device__ __forceinline__ uint32_t xxh32_quad_acc(const uint8_t* p, uint32_t n16, uint32_t steps, uint32_t seed,
+                                                   uint32_t a) {
+    uint32_t v = a == 0 ? seed + kP1 + kP2 : a == 1 ? seed + kP2 : a == 2 ? seed : seed - kP1;
+    if (steps == 0) return v;
+    const uint32_t last = n16 > 0 ? n16 - 1 : 0;   // loads past the item are clamped to its last stripe
+    gu32* q = (gu32*)(uintptr_t)(p + 4 * a);
+    uint32_t A[kXQ], B[kXQ];
+#pragma unroll
+    for (int k = 0; k < kXQ; ++k) A[k] = q[4 * min((uint32_t)k, last)];
+    for (uint32_t s = 0; s < steps; s += 2 * kXQ) {
+#pragma unroll
+        for (int k = 0; k < kXQ; ++k) B[k] = q[4 * min(s + kXQ + (uint32_t)k, last)];
+        __builtin_amdgcn_sched_barrier(0);   // the loads stay ahead of the consumption below
+#pragma unroll
+        for (int k = 0; k < kXQ; ++k) {
+            const uint32_t y = xround(v, A[k]);
+            v = s + (uint32_t)k < n16 ? y : v;
+        }
+        if (s + kXQ >= steps) break;
+#pragma unroll
+        for (int k = 0; k < kXQ; ++k) A[k] = q[4 * min(s + 2 * kXQ + (uint32_t)k, last)];
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int k = 0; k < kXQ; ++k) {
+            const uint32_t y = xround(v, B[k]);
+            v = s + kXQ + (uint32_t)k < n16 ? y : v;
+        }
+    }
+    return v;
+}
+
+// The item's hash from its quad's four accumulators (quad lane 0 gets the
+// result; xxhash.c:370-389): merge, length, tail, avalanche.
+__device__ __forceinline__ uint32_t xxh32_quad_finish(uint32_t v, const uint8_t* p, int64_t len, uint32_t seed) {
+    const uint32_t v1 = __builtin_amdgcn_mov_dpp(v, 0x55, 0xF, 0xF, false);   // quad_perm [1,1,1,1]
+    const uint32_t v2 = __builtin_amdgcn_mov_dpp(v, 0xAA, 0xF, 0xF, false);   // [2,2,2,2]
+    const uint32_t v3 = __builtin_amdgcn_mov_dpp(v, 0xFF, 0xF, 0xF, false);   // [3,3,3,3]
+    const int64_t n16 = len >> 4;
+    uint32_t h = n16 > 0 ? rotl32(v, 1) + rotl32(v1, 7) + rotl32(v2, 12) + rotl32(v3, 18) : seed + kP5;
+    h += (uint32_t)len;
+    return xfinish(h, p + 16 * n16, (int)(len - 16 * n16));
+}
+
+// the wave's largest value of x (uniform)
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) x = max(x, (uint32_t)__shfl_xor((int)x, d));
+    return x;
+}
+
 }  // namespace lz4m

@@ -15,6 +15,23 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: long-running")
 
 
+@pytest.fixture(scope="session", autouse=True)
+def single_call_worker_clean():
+    """Session-end check: no single call of the whole run was
+    handed from the persistent worker kernel to the launch path -- a missed
+    1 s deadline, a stream error, more than three restarts, a failed start or
+    a lone-block staging wait that gave up (lz4m_host.hip g_worker_failures).
+    A worker that stalls cannot hide behind the fallback's correct bytes."""
+    yield
+    nat = sys.modules.get("lz4._native")
+    if nat is None or getattr(nat, "_lib", None) is None:
+        return   # the library never loaded (CPU-only run)
+    import ctypes
+    st = (ctypes.c_uint32 * 16)()
+    failures = nat.lib().lz4m_single_call_worker_state(st)
+    assert failures == 0, f"{failures} single call(s) fell back from the worker to the launch path"
+
+
 @pytest.fixture(scope="session")
 def oracle():
     import oracle as O

@@ -214,6 +214,28 @@ def test_xxh32_batch(gpu, oracle, corpus):
         assert got == [oracle.xxh32(b, seed) for b in items]
 
 
+def test_xxh32_batch_page(gpu, oracle):
+    """The quad-per-item batch kernel on a config-5-like page: 4 101 items
+    (not a multiple of the 16 items a wave takes) of 0..70 000 bytes at any
+    alignment, overlapping slices of one buffer, wave-mates of very different
+    lengths (items with no full stripe next to 64 KiB ones), against the
+    oracle's XXH32 (xxhash.c:392-416)."""
+    rng = np.random.default_rng(5)
+    buf = rng.integers(0, 256, 8 << 20, dtype=np.uint8)
+    n = 4101
+    lens = rng.integers(0, 70000, n)
+    lens[rng.integers(0, n, 300)] = rng.integers(0, 16, 300)   # tails only
+    lens[:16] = [0, 1, 15, 16, 17, 31, 32, 33, 65536, 3, 70000, 0, 48, 49, 1000, 5]
+    offs = rng.integers(0, len(buf) - 70000, n)
+    d = torch.from_numpy(buf).to(gpu)
+    out = torch.empty(n, dtype=torch.int32, device=gpu)
+    N.launch_xxh32_batch(d, torch.tensor(offs, dtype=torch.int64, device=gpu),
+                         torch.tensor(lens, dtype=torch.int64, device=gpu), 0x1234567, out, n)
+    got = [v & 0xFFFFFFFF for v in out.cpu().tolist()]
+    want = [oracle.xxh32(buf[o:o + k].tobytes(), 0x1234567) for o, k in zip(offs, lens)]
+    assert got == want
+
+
 @pytest.mark.parametrize("n", [0, 1, 15, 16, 17, 63, 64, 511, 512, 513, 1023, 1024, 1025, 4096 + 7,
                                3 * 65536 + 5, (1 << 20) + 77])
 @pytest.mark.parametrize("shift", [0, 1, 3, 4])

@@ -64,3 +64,76 @@ def test_host_copy_in_forked_child():
         os._exit(0 if np.array_equal(d2, src) else 1)
     _, status = os.waitpid(pid, 0)
     assert os.WIFEXITED(status) and os.WEXITSTATUS(status) == 0
+
+
+def _copy_many(lib, srcs, threads, null_empty=True):
+    """lz4m_host_copy_many over numpy sources; empty items get NULL pointers
+    (as lz4.block.compress_many passes for empty bytes)."""
+    dsts = [np.full(len(s), 0xA5, dtype=np.uint8) for s in srcs]
+    n = len(srcs)
+    D = (C.c_void_p * max(n, 1))()
+    S = (C.c_void_p * max(n, 1))()
+    L = (C.c_size_t * max(n, 1))()
+    for i, (d, s) in enumerate(zip(dsts, srcs)):
+        empty = len(s) == 0 and null_empty
+        D[i] = None if empty else d.ctypes.data
+        S[i] = None if empty else s.ctypes.data
+        L[i] = len(s)
+    lib.lz4m_host_copy_many(D, S, L, n, threads)
+    return dsts
+
+
+def _rand_items(rng, sizes):
+    return [rng.integers(0, 256, int(k), dtype=np.uint8) for k in sizes]
+
+
+@pytest.mark.parametrize("threads", [1, 2, 3, 16])
+@pytest.mark.parametrize("case", ["empty_null", "fewer_than_threads", "skewed", "just_below_4mib",
+                                  "just_above_4mib", "one_huge", "zero_items"])
+def test_host_copy_many_matches_per_item_copy(case, threads):
+    """lz4m_host_copy_many (the packing and unpacking of compress_many /
+    decompress_many, lz4m_host_copy.c) equals a per-item copy: empty items
+    with NULL pointers, fewer items than threads, heavily skewed sizes, totals
+    on both sides of the 4 MiB threading threshold, one item larger than
+    total / threads."""
+    import lz4._native as N
+    lib = N.lib()
+    rng = np.random.default_rng(hash(case) & 0xFFFF)
+    sizes = {
+        "empty_null": [0, 5, 0, 0, 70000, 0, 1, 0] * 40,
+        "fewer_than_threads": [3 << 20, 2 << 20],
+        "skewed": [1, 2, 3, 9 << 20, 4, 0, 5, 1 << 20, 7, 11],
+        "just_below_4mib": [(1 << 20) - 1, 1 << 20, 1 << 20, (1 << 20) - 2],
+        "just_above_4mib": [(1 << 20) + 1, 1 << 20, 1 << 20, (1 << 20) + 2],
+        "one_huge": [12 << 20] + [100] * 50,
+        "zero_items": [],
+    }[case]
+    srcs = _rand_items(rng, sizes)
+    dsts = _copy_many(lib, srcs, threads)
+    for s, d in zip(srcs, dsts):
+        assert np.array_equal(s, d)
+
+
+def test_host_copy_many_from_many_threads():
+    """Concurrent lz4m_host_copy_many calls from several host threads share
+    one pool (calls are serialised inside it) and all copy exactly."""
+    import lz4._native as N
+    lib = N.lib()
+    bad = []
+
+    def work(k):
+        rng = np.random.default_rng(100 + k)
+        for _ in range(3):
+            sizes = rng.integers(0, 1 << 20, 12)
+            sizes[rng.integers(0, 12, 3)] = 0
+            srcs = _rand_items(rng, sizes)
+            for s, d in zip(srcs, _copy_many(lib, srcs, 8)):
+                if not np.array_equal(s, d):
+                    bad.append(k)
+
+    ts = [threading.Thread(target=work, args=(k,)) for k in range(6)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=120)
+    assert not bad
