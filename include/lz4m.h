@@ -135,9 +135,6 @@ const char* lz4m_version_string(void);
  *             block with its recent output in LDS, then an exact lane-per-block
  *             finisher for each block's tail (needs the scratch of
  *             lz4m_decompress_workspace_size);
- *   resident -- large batches: the rows decoder's parse and finisher around
- *             a block-resident executor (one 256-thread workgroup per block,
- *             the block's whole output in LDS, no match source read from HBM);
  *   hist   -- one wavefront per block with its recent output in LDS (small and
  *             mid-size batches, large blocks, and any batch without scratch);
  * This entry point takes no scratch, so it always uses the hist decoder; pass
@@ -169,11 +166,10 @@ int lz4m_decompress_batch_ws(const uint8_t* d_src, const int64_t* d_src_off, con
                              lz4m_stream_t stream);
 
 /* lz4m_decompress_batch_ws with an explicit decoder (tests, A/B runs); any
- * other id (1, 2, 5 and 6 were retired decoders) returns LZ4M_EINVAL. */
+ * other id (1, 2, 5, 6 and 7 were retired decoders) returns LZ4M_EINVAL. */
 #define LZ4M_DECODER_AUTO   0
 #define LZ4M_DECODER_HIST   3
 #define LZ4M_DECODER_ROWS   4
-#define LZ4M_DECODER_RESIDENT 7
 int lz4m_decompress_batch_sel(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len,
                               uint8_t* d_dst, const int64_t* d_dst_off, const int32_t* d_dst_cap,
                               int32_t* d_status, int64_t n, void* d_work, size_t work_bytes, int decoder,

@@ -1353,7 +1353,7 @@ int env_int(const char* name, int dflt) {
 
 // the values are the C-ABI's decoder ids (include/lz4m.h); 1, 2, 5 and 6
 // were retired decoders and are rejected
-enum Decoder { kAuto = 0, kHistDec = 3, kRowsDec = 4, kResDec = 7 };
+enum Decoder { kAuto = 0, kHistDec = 3, kRowsDec = 4 };   // 7 was the block-resident experiment (removed round 5)
 
 // LZ4M_DECODER forces a decoder (A/B measurements, tests): hist | rows;
 // unset = by batch size and scratch.
@@ -1363,7 +1363,6 @@ int decoder_env() {
         if (e == nullptr) return (int)kAuto;
         if (strcmp(e, "hist") == 0) return (int)kHistDec;
         if (strcmp(e, "rows") == 0) return (int)kRowsDec;
-        if (strcmp(e, "resident") == 0) return (int)kResDec;
         return (int)kAuto;
     }();
     return mode;
@@ -1383,7 +1382,7 @@ extern "C" int lz4m_decompress_batch_sel(const uint8_t* d_src, const int64_t* d_
                                          uint8_t* d_dst, const int64_t* d_dst_off, const int32_t* d_dst_cap,
                                          int32_t* d_status, int64_t n, void* d_work, size_t work_bytes, int decoder,
                                          lz4m_stream_t stream) {
-    if (n < 0 || !(decoder == kAuto || decoder == kHistDec || decoder == kRowsDec || decoder == kResDec))
+    if (n < 0 || !(decoder == kAuto || decoder == kHistDec || decoder == kRowsDec))
         return LZ4M_EINVAL;
     if (n == 0) return 0;
     hipStream_t st = (hipStream_t)stream;
@@ -1398,16 +1397,11 @@ extern "C" int lz4m_decompress_batch_sel(const uint8_t* d_src, const int64_t* d_
     static const int rows_min = env_int("LZ4M_ROWS_MIN_BLOCKS", 32768);   // crossover measured, DESIGN 3.1
     if (decoder == kAuto) decoder = rows_fit && n >= rows_min ? kRowsDec : kHistDec;
     if (decoder != kHistDec && !rows_fit) decoder = kHistDec;
-    if (decoder == kRowsDec || decoder == kResDec) {
+    if (decoder == kRowsDec) {
         int pg = 1, eg = 1;
         lz4m_rows_grids(n, &pg, &eg);
-        int rc = 0;
-        if (decoder == kResDec) {
-            rc = lz4m_rows_parse_launch(d_src, d_src_off, d_src_len, d_dst_cap, n, d_work, work_bytes, pg, st);
-            if (rc == 0) rc = lz4m_resident_exec_launch(d_src, d_src_off, d_src_len, d_dst, d_dst_off, n, d_work, work_bytes, st);
-        } else {
-            rc = lz4m_rows_launch(d_src, d_src_off, d_src_len, d_dst, d_dst_off, d_dst_cap, n, d_work, work_bytes, pg, eg, st);
-        }
+        const int rc = lz4m_rows_launch(d_src, d_src_off, d_src_len, d_dst, d_dst_off, d_dst_cap, n, d_work, work_bytes,
+                                        pg, eg, st);
         if (rc != 0) return rc;
         const RowMeta* meta = reinterpret_cast<const RowMeta*>(static_cast<const uint8_t*>(d_work) + kRowsMeta);
         const int64_t grid = (n + 255) / 256;

@@ -34,14 +34,6 @@ extern "C" {
 size_t lz4m_rows_fixed_bytes(int64_t n);
 // persistent grid sizes for the two kernels on the current device
 int lz4m_rows_grids(int64_t n, int* parse_grid, int* exec_grid);
-// the parse kernel alone (counters zeroed first)
-int lz4m_rows_parse_launch(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len,
-                           const int32_t* d_dst_cap, int64_t n, void* d_work, size_t work_bytes, int parse_grid,
-                           hipStream_t stream);
-// the block-resident executor (lz4m_resident.hip) after lz4m_rows_parse_launch
-int lz4m_resident_exec_launch(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len,
-                              uint8_t* d_dst, const int64_t* d_dst_off, int64_t n, void* d_work, size_t work_bytes,
-                              hipStream_t stream);
 // parse + row execution; the finisher is launched by the caller afterwards
 int lz4m_rows_launch(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len, uint8_t* d_dst,
                      const int64_t* d_dst_off, const int32_t* d_dst_cap, int64_t n, void* d_work, size_t work_bytes,

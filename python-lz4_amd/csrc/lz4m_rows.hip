@@ -306,6 +306,10 @@ __device__ __forceinline__ const uint8_t* readlane_safe_ptr(uint64_t a) {
     typedef __attribute__((address_space(1))) const uint8_t gu8;
     return (const uint8_t*)(gu8*)(uintptr_t)a;
 }
+#ifndef LZ4M_PARSE_RUNCAP
+#define LZ4M_PARSE_RUNCAP 16            // length-byte runs longer than this end the good prefix (finisher)
+#endif
+constexpr int32_t kPRunCap = LZ4M_PARSE_RUNCAP;
 #ifndef LZ4M_PARSE_MIN_ACTIVE
 #define LZ4M_PARSE_MIN_ACTIVE 40        // run the general step once fewer lanes than this can go on
 #endif
@@ -463,11 +467,16 @@ __global__ __launch_bounds__(kPWG) void rows_parse_kernel(const uint8_t* __restr
                     good = false;
                 } else {
                     uint32_t b;
+                    int32_t run = 0;
                     do {
                         b = PB(q);
                         ++q;
                         lit += b;
                         if (q > iend - 15) good = false;
+                        // a run past kPRunCap bytes (a literal of >= 4 KiB: an
+                        // incompressible block's single literal is ~257) goes to
+                        // the finisher: not read byte by byte here, mostly from HBM
+                        if (++run >= kPRunCap && b == 255) good = false;
                     } while (good && b == 255);
                     if (good && (op + lit > oend - 32 || q + lit > iend - 32)) good = false;   // :2016-2027
                 }
@@ -483,11 +492,13 @@ __global__ __launch_bounds__(kPWG) void rows_parse_kernel(const uint8_t* __restr
                 ml = tok & 15;
                 if (ml == 15) {   // read_variable_length(&ip, iend - 4, 0)
                     uint32_t b;
+                    int32_t run = 0;
                     do {
                         b = PB(pe);
                         ++pe;
                         ml += b;
                         if (pe > iend - 4) good = false;
+                        if (++run >= kPRunCap && b == 255) good = false;   // (as above)
                     } while (good && b == 255);
                 }
                 ml += 4;
@@ -630,8 +641,12 @@ constexpr int32_t kRowsH = LZ4M_ROWS_H;
 #ifndef LZ4M_ROWS_PASS1
 #define LZ4M_ROWS_PASS1 0     // A/B: a first readiness pass without the row scans (sources before the round)
 #endif
+#ifndef LZ4M_ROWS_ORDER
+#define LZ4M_ROWS_ORDER 1   // 1 (required: FarSrc is shared by P and Q): parse ahead after this round's passes
+#endif
+static_assert(LZ4M_ROWS_ORDER == 1, "the far-source pieces (FarSrc) are reused by the round parsed ahead");
 #ifndef LZ4M_ROWS_XP
-#define LZ4M_ROWS_XP 0      // timing probes (bits 2, 4, 8 give WRONG output): 1 sync-path drain, 2 no HBM loads in passes, 4 no late loads, 8 no far prefetch
+#define LZ4M_ROWS_XP 0      // timing probes, WRONG output (r05a): 2 no HBM loads in passes, 4 no late loads, 8 no far prefetch
 #endif
 #ifndef LZ4M_ROWS_COUNTED
 #define LZ4M_ROWS_COUNTED 0   // A/B: a fixed number of memory operations per round on the common path (measured -1 %)
@@ -688,12 +703,20 @@ __device__ __forceinline__ void load32(const uint8_t* s, int32_t t, int32_t iend
 // previous one executes, and the registers it frees hold the executor at 5
 // waves per SIMD (1 KiB histories).
 struct PSeq {
-    u32x4 pre0;                       // the far source's first 16 bytes, requested
     int32_t t, lit, off, ml, o, dlt;  // t: the literal's input position
     int32_t opn, ipn;                 // uniform across the row
     uint32_t fl;                      // flags | (use << 8): the row takes its first `use` lanes
 };
 constexpr uint32_t kFlU = 1, kFlFar = 2, kFlLate = 4, kFlLitHbm = 8;
+
+// The far source's first 32 bytes, requested when the round is parsed (two
+// 16-byte pieces; the second only where a far match is longer than 16 bytes)
+// and consumed by the round's passes.  Kept outside PSeq: after the passes
+// the same registers take the next round's requests, with no copy between --
+// a copy of a register with a load in flight waits for that load.
+struct FarSrc {
+    u32x4 g0, g1;
+};
 
 // Parse the row's round at (k0, ip, op): lane jj's length byte dlt, its
 // start t and its 32 input bytes wa|wb (wb is clamped into the block, so
@@ -702,7 +725,8 @@ constexpr uint32_t kFlU = 1, kFlFar = 2, kFlLate = 4, kFlLitHbm = 8;
 // below F (flushed), else marked late (requested once flushed).
 __device__ __forceinline__ void parse_round(PSeq& P, int32_t jj, int32_t r, int32_t k0, int32_t nseq, int32_t ip,
                                             int32_t op, int32_t bnext, int32_t F, const uint8_t* s, const uint8_t* d,
-                                            int32_t iend, int32_t dlt, int32_t t, u32x4 wa, u32x4 wb, lds_u32x4* XS) {
+                                            int32_t iend, int32_t dlt, int32_t t, u32x4 wa, u32x4 wb, lds_u32x4* XS,
+                                            FarSrc& FS) {
     const bool act = k0 + jj < nseq;
     const bool esc = dlt == 255;   // length >= 255: the parse left it to be re-parsed
     const bool wbok = t + 32 <= iend;
@@ -753,8 +777,13 @@ __device__ __forceinline__ void parse_round(PSeq& P, int32_t jj, int32_t r, int3
     const bool late = far & (s0 + 32 > F);
     const bool pf = far & !late;
     // unconditional requests (lanes without a far source read the block start)
-    if (LZ4M_ROWS_XP & 8) P.pre0 = u32x4{(uint32_t)s0, 0, 0, 0};
-    else P.pre0 = ld16(d + (pf ? s0 : 0));
+    if (LZ4M_ROWS_XP & 8) {
+        FS.g0 = FS.g1 = u32x4{(uint32_t)s0, 0, 0, 0};
+    } else {
+        FS.g0 = ld16(d + (pf ? s0 : 0));
+        // the second piece [s0 + 16, s0 + 32) is flushed too (not late: s0 + 32 <= F)
+        FS.g1 = ld16(d + (pf & (ml > 16) ? s0 + 16 : 0));
+    }
     const uint32_t sh = (uint32_t)lp;
     XS[0] = u32x4{__builtin_amdgcn_alignbyte(wa.y, wa.x, sh), __builtin_amdgcn_alignbyte(wa.z, wa.y, sh),
                  __builtin_amdgcn_alignbyte(wa.w, wa.z, sh), __builtin_amdgcn_alignbyte(wb.x, wa.w, sh)};
@@ -804,13 +833,15 @@ __device__ __forceinline__ void load_in(const uint8_t* s, int32_t t, int32_t ien
     a = ld16s(s + ta);
     b = ld16s(s + tb);
 }
+// (no select on the loaded value: a lane past the block's good sequences
+// reads the last length, and parse_round masks it by `act`; a select here
+// waited for the load at once)
 __device__ __forceinline__ int32_t load_len(const uint8_t* dl, int32_t k, int32_t nseq) {
 #if LZ4M_ROWS_NT
-    const int32_t v = (int32_t)__builtin_nontemporal_load(dl + (k < nseq ? k : nseq - 1));
+    return (int32_t)__builtin_nontemporal_load(dl + (k < nseq ? k : nseq - 1));
 #else
-    const int32_t v = (int32_t)dl[k < nseq ? k : nseq - 1];
+    return (int32_t)dl[k < nseq ? k : nseq - 1];
 #endif
-    return k < nseq ? v : 0;
 }
 
 #if LZ4M_LDS_ALIGN
@@ -865,8 +896,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LZ4M_ROWS_WA
     int32_t iend = 0, nseq = 0, k0 = 0, ip = 0, op = 0, base = 0, F = 0;
     bool have = false, sync = true;
     PSeq P, Q;   // P: the round to execute; Q: the next one, parsed ahead
-    // inputs of the round after Q: start tn, bytes na|nb, length dn; dnn = the one after
-    int32_t dn = 0, dnn = 0;
+    FarSrc FS;   // P's far-source pieces (after P's passes: Q's)
+    // the round after P (parsed next): its length bytes as their inclusive row
+    // prefix sum incq (a computed value) and its 32 input bytes na|nb; lraw =
+    // the raw length bytes of the round after that.  Every loaded value is
+    // consumed before the same variable is loaded again, so none is copied
+    // across the loop edge (a copy of a register with a load in flight waits
+    // for it -- in order, for every younger request too: r05)
+    int32_t incq = 0, lraw = 0;
     u32x4 na = u32x4{0, 0, 0, 0}, nb = na;
     RP_DECL
     while (true) {
@@ -904,12 +941,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LZ4M_ROWS_WA
             const int32_t tc = ip + row_incl_sum(dc) - dc;
             u32x4 wa, wb;
             load_in(s, tc, iend, wa, wb);
-            parse_round(P, jj, r, k0, nseq, ip, op, base, F, s, d, iend, dc, tc, wa, wb, XSL);
-            dn = load_len(dl, k0 + 16 + jj, nseq);
-            load_in(s, P.ipn + row_incl_sum(dn) - dn, iend, na, nb);
-            dnn = load_len(dl, k0 + 32 + jj, nseq);
+            parse_round(P, jj, r, k0, nseq, ip, op, base, F, s, d, iend, dc, tc, wa, wb, XSL, FS);
+            const int32_t dq = load_len(dl, k0 + 16 + jj, nseq);
+            incq = row_incl_sum(dq);
+            load_in(s, P.ipn + incq - dq, iend, na, nb);
+            lraw = load_len(dl, k0 + 32 + jj, nseq);
             sync = false;
-            if (LZ4M_ROWS_XP & 1) wait_vm0();
+            // the loads just issued (this round's far sources among them) are
+            // waited for here, once: left pending, the merge of this rare path
+            // with the common one made every round wait for its newest
+            // far-source request (r05a: -1.7 %)
+            wait_vm0();
 #if LZ4M_ROWS_COUNTED
             wait_vm0();   // (rare: block starts, short rounds) the common path's waits stay counted
 #endif
@@ -997,15 +1039,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LZ4M_ROWS_WA
         }
         }
         // ---- parse the next round ahead (its far sources are requested now),
-        // then request the inputs of the round after it
+        // then request the inputs of the round after it.  LZ4M_ROWS_ORDER 1:
+        // after this round's passes, so that no load the passes wait on (a
+        // long far match's later pieces, a late source) is younger than these
+        // requests -- gfx9 counts loads in order, and waiting for one load
+        // waits for every older one
         const bool ahead = (P.fl >> 8) == 16 && k0 + 16 < nseq;
-        if (ahead) {
-            const int32_t bq = next_base(P.opn, base);
-            parse_round(Q, jj, r, k0 + 16, nseq, P.ipn, P.opn, bq, F, s, d, iend, dn, P.ipn + row_incl_sum(dn) - dn, na, nb, XSL);
-            dn = dnn;
-            load_in(s, Q.ipn + row_incl_sum(dn) - dn, iend, na, nb);
-            dnn = load_len(dl, k0 + 48 + jj, nseq);
-        }
+        auto parse_ahead = [&]() __attribute__((always_inline)) {
+            if (ahead) {
+                const int32_t bq = next_base(P.opn, base);
+                // Q's length bytes from their prefix sum: lane j's minus lane j-1's
+                const int32_t dq = incq - __builtin_amdgcn_update_dpp(0, incq, 0x111, 0xF, 0xF, true);
+                parse_round(Q, jj, r, k0 + 16, nseq, P.ipn, P.opn, bq, F, s, d, iend, dq, P.ipn + incq - dq, na, nb, XSL, FS);
+                incq = row_incl_sum(lraw);
+                load_in(s, Q.ipn + incq - lraw, iend, na, nb);
+                lraw = load_len(dl, k0 + 48 + jj, nseq);
+            }
+        };
+        if (!LZ4M_ROWS_ORDER) parse_ahead();
         RP_MARK(11);
         // ---- execute round P
         const bool u = (P.fl & kFlU) != 0;
@@ -1015,8 +1066,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LZ4M_ROWS_WA
         // readiness passes: a match is copied once no earlier pending match of
         // the round writes into its source [s0, se)
         const bool far = (P.fl & kFlFar) != 0, late = (P.fl & kFlLate) != 0;
-        u32x4 g0 = P.pre0;
-            if (!(LZ4M_ROWS_XP & 4) && __any(late)) {   // a source flushed only by the previous round (rare): load it now
+        u32x4 g0 = FS.g0;
+        const u32x4 g1 = FS.g1;
+        if (!(LZ4M_ROWS_XP & 4) && __any(late)) {   // a source flushed only by the previous round (rare): load it now
             const u32x4 lv = ld16(d + (late ? s0 : 0));
             g0 = late ? lv : g0;
 #if LZ4M_ROWS_COUNTED
@@ -1025,7 +1077,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LZ4M_ROWS_WA
         }
         const int32_t se = s0 + (off < ml ? off : ml);
         const bool per = off < 16;   // period pattern (s0 >= base here: m - base >= off)
-        const int32_t stp = per ? 16 - (16 % off) : 16;
+        // 16 - 16 % off for off 1..15 from a table (3 bits per offset; the
+        // integer division was ~20 VALU per round)
+        constexpr uint64_t kRem16 = (0ull << 3) | (0ull << 6) | (1ull << 9) | (0ull << 12) | (1ull << 15) |
+                                    (4ull << 18) | (2ull << 21) | (0ull << 24) | (7ull << 27) | (6ull << 30) |
+                                    (5ull << 33) | (4ull << 36) | (3ull << 39) | (2ull << 42) | (1ull << 45);
+        const int32_t stp = per ? 16 - (int32_t)((kRem16 >> (3u * ((uint32_t)off & 15u))) & 7u) : 16;
         bool pend = u;
 #if LZ4M_ROWS_PUTMASK >= 3
         // one match copy (exec-masked to the ready lanes: an LDS access costs per active lane)
@@ -1039,9 +1096,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LZ4M_ROWS_WA
                     u32x4 v = v0;
                     if (!per) {
                         const int32_t sp = s0 + i;
-                        // sp < base: flushed (F >= base + kRowsKeep - 16)
-                        if (LZ4M_ROWS_XP & 2) v = lds_ld16u(HB + (sp >= base ? sp - base : 0));
-                        else v = sp >= base ? lds_ld16u(HB + (sp - base)) : ld16(d + sp);
+                        // sp < base: flushed (F >= base + kRowsKeep - 16); the
+                        // second piece of a (not late) far source was requested
+                        // with the first; later pieces are loaded now, only where
+                        // some lane needs one (this wait then covers only loads
+                        // older than the round's own requests, LZ4M_ROWS_ORDER)
+                        v = lds_ld16u(HB + (sp >= base ? sp - base : 0));
+                        if (!(LZ4M_ROWS_XP & 2)) {
+                            const bool pc1 = (i == 16) & far & !late;
+                            if (sp < base && pc1) v = g1;
+                            const bool hb = (sp < base) & !pc1;
+                            if (__any(hb)) {
+                                const u32x4 x = ld16(d + (hb ? sp : 0));
+                                v = hb ? x : v;
+                            }
+                        }
                     }
                     LDS_PUT(HB + (m - base + i), v, ml - i);
                 }
@@ -1099,6 +1168,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LZ4M_ROWS_WA
             pend = pend && !ready;
         }
 #endif
+        if (LZ4M_ROWS_ORDER) parse_ahead();
         RP_MARK(13);
         // ---- flush, advance, rebase for the next round
         const int32_t opn = P.opn;
@@ -1179,24 +1249,6 @@ extern "C" int lz4m_rows_launch(const uint8_t* d_src, const int64_t* d_src_off, 
                        d_src_len, d_dst_cap, n, meta, lens, lens_cap, ctr);
     hipLaunchKernelGGL(rows_exec_kernel, dim3((uint32_t)exec_grid), dim3(64), 0, stream, d_src, d_src_off, d_src_len,
                        d_dst, d_dst_off, meta, lens, n, ctr);
-    return (int)hipGetLastError();
-}
-
-// the parse alone (counters zeroed first): the block-resident executor
-// (lz4m_resident.hip) reads the same records and length bytes
-extern "C" int lz4m_rows_parse_launch(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len,
-                                      const int32_t* d_dst_cap, int64_t n, void* d_work, size_t work_bytes,
-                                      int parse_grid, hipStream_t stream) {
-    const size_t fixed = lz4m_rows_fixed_bytes(n);
-    if (work_bytes < fixed) return LZ4M_ROWS_ENOSPACE;
-    unsigned long long* ctr = static_cast<unsigned long long*>(d_work);
-    RowMeta* meta = reinterpret_cast<RowMeta*>(static_cast<uint8_t*>(d_work) + kRowsMeta);
-    uint8_t* lens = static_cast<uint8_t*>(d_work) + fixed;
-    const int64_t lens_cap = (int64_t)(work_bytes - fixed);
-    hipError_t e = hipMemsetAsync(ctr, 0, 64, stream);
-    if (e != hipSuccess) return (int)e;
-    hipLaunchKernelGGL(rows_parse_kernel, dim3((uint32_t)parse_grid), dim3(kPWG), 0, stream, d_src, d_src_off,
-                       d_src_len, d_dst_cap, n, meta, lens, lens_cap, ctr);
     return (int)hipGetLastError();
 }
 

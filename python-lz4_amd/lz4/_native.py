@@ -32,7 +32,7 @@ LINKED_SERIAL = 1        # lz4m_compress_linked_batch modes
 LINKED_SPECULATIVE = 2
 EINVAL = 0x10000
 # decoder selector of lz4m_decompress_batch_sel (include/lz4m.h)
-DECODERS = {"auto": 0, "hist": 3, "rows": 4, "resident": 7}
+DECODERS = {"auto": 0, "hist": 3, "rows": 4}
 
 _lock = threading.Lock()
 _lib = None

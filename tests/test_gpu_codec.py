@@ -27,7 +27,7 @@ def _pack(blocks):
 
 # every decoder (include/lz4m.h lz4m_decompress_batch_sel) must give the
 # reference's bytes and statuses; "auto" is the size-based default
-DECODERS = ["auto", "rows", "hist", "resident"]
+DECODERS = ["auto", "rows", "hist"]
 
 
 def gpu_decompress(blocks, caps, dev, decoder="auto"):
@@ -340,7 +340,7 @@ def _offset0_block(lit, ml):
     return seq + bytes([5 << 4]) + b"tail!"
 
 
-@pytest.mark.parametrize("decoder", ["auto", "hist", "resident"])
+@pytest.mark.parametrize("decoder", ["auto", "hist"])
 def test_decompress_large_batch_edges(gpu, oracle, corpus, decoder):
     """A batch above the small-batch switch-over (32 768 blocks), so the
     default dispatch runs the large-batch decoder, with every edge case of the
