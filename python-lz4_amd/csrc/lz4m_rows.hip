@@ -295,9 +295,6 @@ static_assert(kPStage == 32 || kPStage == 64, "length ring: 32 or 64 entries");
 #define LZ4M_PARSE_WG 64
 #endif
 constexpr int kPWG = LZ4M_PARSE_WG;     // parse workgroup (LDS is allocated per workgroup)
-#ifndef LZ4M_PARSE_PAIR
-#define LZ4M_PARSE_PAIR 0               // A/B: two sequences per fast step (measured -1.5 %)
-#endif
 #ifndef LZ4M_PARSE_COOP
 #define LZ4M_PARSE_COOP 1               // A/B: ring refills loaded by four lanes per block (64-byte requests)
 #endif
@@ -306,6 +303,9 @@ __device__ __forceinline__ const uint8_t* readlane_safe_ptr(uint64_t a) {
     typedef __attribute__((address_space(1))) const uint8_t gu8;
     return (const uint8_t*)(gu8*)(uintptr_t)a;
 }
+#ifndef LZ4M_PARSE_V2
+#define LZ4M_PARSE_V2 1                 // predicated two-step fast loop; ring / length-ring stops skip the general parse; one-extension-byte general parse
+#endif
 #ifndef LZ4M_PARSE_RUNCAP
 #define LZ4M_PARSE_RUNCAP 16            // length-byte runs longer than this end the good prefix (finisher)
 #endif
@@ -344,7 +344,7 @@ __global__ __launch_bounds__(kPWG) void rows_parse_kernel(const uint8_t* __restr
     int64_t idx = -1, loff = 0;
     int32_t iend = 0, oend = 0, ip = 0, op = 0, k = 0, kf = 0, wb = 0;
     u32x4 pf[4];   // stream bytes [wb + 128, wb + 192), requested ahead
-    bool live = false, need = false, more = true, pfv = false;
+    bool live = false, need = false, more = true, pfv = false, stall = false;
     RP_DECL
     while (true) {
         RP_MARK(2);
@@ -443,6 +443,13 @@ __global__ __launch_bounds__(kPWG) void rows_parse_kernel(const uint8_t* __restr
             pfv = false;
         }
 #endif
+#if LZ4M_PARSE_V2
+        // a lane stopped at its ring's end that the rotation could not serve
+        // (nothing requested: the ring already ends at the input's end) takes
+        // the general parse; every other stopped lane retries the fast loop
+        if (live && stall && !need && ip + 16 > wb + kPW) need = true;
+        stall = false;
+#endif
         if (live && need) {
             need = false;
             if (ip + 32 > wb + kPW) {   // no bytes ahead (block start, a long literal): load the ring now
@@ -456,58 +463,117 @@ __global__ __launch_bounds__(kPWG) void rows_parse_kernel(const uint8_t* __restr
                 pfv = false;
             }
             // one sequence, general parse with the reference fast loop's tests
-            // (lz4.c:2004-2086); bytes outside the ring come from HBM
-#define PB(x) ((x) - wb < kPW ? (uint32_t)W[(x) & (kPW - 1)] : (uint32_t)s[(x)])
-            bool good = true;
-            const uint32_t tok = PB(ip);
-            int64_t lit = tok >> 4;
-            int32_t q = ip + 1;
-            if (lit == 15) {   // read_variable_length(&ip, iend - 15, 1), lz4.c:1903-1928
-                if (q >= iend - 15) {
-                    good = false;
-                } else {
-                    uint32_t b;
-                    int32_t run = 0;
-                    do {
-                        b = PB(q);
-                        ++q;
-                        lit += b;
-                        if (q > iend - 15) good = false;
-                        // a run past kPRunCap bytes (a literal of >= 4 KiB: an
-                        // incompressible block's single literal is ~257) goes to
-                        // the finisher: not read byte by byte here, mostly from HBM
-                        if (++run >= kPRunCap && b == 255) good = false;
-                    } while (good && b == 255);
-                    if (good && (op + lit > oend - 32 || q + lit > iend - 32)) good = false;   // :2016-2027
-                }
-            } else if (q > iend - 17) {   // :2034
-                good = false;
-            }
+            // (lz4.c:2004-2086)
+            bool good = true, slow = true;
             int32_t pe = 0;
-            int64_t ml = 0;
-            if (good) {
-                const int32_t po = q + (int32_t)lit;
-                const uint32_t off = PB(po) | (PB(po + 1) << 8);
-                pe = po + 2;
-                ml = tok & 15;
-                if (ml == 15) {   // read_variable_length(&ip, iend - 4, 0)
-                    uint32_t b;
-                    int32_t run = 0;
-                    do {
-                        b = PB(pe);
-                        ++pe;
-                        ml += b;
-                        if (pe > iend - 4) good = false;
-                        if (++run >= kPRunCap && b == 255) good = false;   // (as above)
-                    } while (good && b == 255);
+            int64_t lit = 0, ml = 0;
+#if LZ4M_PARSE_V2
+            // straight-line from the 32 ring bytes at ip (the ring holds them:
+            // loaded above if not): literal and match lengths with at most one
+            // extension byte each, offset inside the 32 bytes -- the same
+            // tests, in the same order, as the byte loop below, which takes
+            // only what this cannot (a 255 extension byte, a literal of more
+            // than 27 bytes)
+            {
+                const u32x4 w0 = ring_ld16(W, ip & (kPW - 1)), w1 = ring_ld16(W, (ip + 16) & (kPW - 1));
+                const uint32_t tok = w0.x & 0xFFu;
+                const int32_t l0 = (int32_t)(tok >> 4), mlc = (int32_t)(tok & 15u);
+                int32_t q = 1, L = l0;
+                bool g = true, sl = false;
+                if (l0 == 15) {   // read_variable_length(&ip, iend - 15, 1), one byte of it
+                    if (ip + 1 >= iend - 15) {
+                        g = false;
+                    } else {
+                        const int32_t e = (int32_t)((w0.x >> 8) & 0xFFu);
+                        q = 2;
+                        L += e;
+                        if (ip + 2 > iend - 15) g = false;
+                        else if (e == 255) sl = true;
+                        if (g && !sl && (op + L > oend - 32 || ip + q + L > iend - 32)) g = false;   // :2016-2027
+                    }
+                } else if (ip + 1 > iend - 17) {   // :2034
+                    g = false;
                 }
-                ml += 4;
-                // offset 0 and offsets before the block start go to the exact
-                // path (lz4.c:2071, :2081); so do matches reaching oend - 64 (:2073, :2076)
-                if (good && (off == 0 || (int64_t)off > (int64_t)op + lit || (int64_t)op + lit + ml >= (int64_t)oend - 64))
-                    good = false;
+                int32_t M = mlc, pq = 0;
+                if (g && !sl) {
+                    const int32_t po = q + L;   // the offset's byte in the 32
+                    if (po + 3 > 32) {
+                        sl = true;
+                    } else {
+                        const uint32_t dw = dword32(w0, w1, (uint32_t)(po > 28 ? 28 : po)) >> (8u * (uint32_t)(po > 28 ? po - 28 : 0));
+                        const int32_t off = (int32_t)(dw & 0xFFFFu);
+                        pq = po + 2;
+                        if (mlc == 15) {   // read_variable_length(&ip, iend - 4, 0), one byte of it
+                            const int32_t e2 = (int32_t)((dw >> 16) & 0xFFu);
+                            ++pq;
+                            M += e2;
+                            if (ip + pq > iend - 4) g = false;
+                            else if (e2 == 255) sl = true;
+                        }
+                        M += 4;
+                        if (g && !sl && (off == 0 || off > op + L || op + L + M >= oend - 64)) g = false;
+                    }
+                }
+                slow = sl;
+                if (!sl) {
+                    good = g;
+                    pe = ip + pq;
+                    lit = L;
+                    ml = M;
+                }
             }
+#endif
+            if (slow) {   // (LZ4M_PARSE_V2: rare) byte by byte; bytes outside the ring come from HBM
+#define PB(x) ((x) - wb < kPW ? (uint32_t)W[(x) & (kPW - 1)] : (uint32_t)s[(x)])
+                good = true;
+                const uint32_t tok = PB(ip);
+                lit = tok >> 4;
+                int32_t q = ip + 1;
+                if (lit == 15) {   // read_variable_length(&ip, iend - 15, 1), lz4.c:1903-1928
+                    if (q >= iend - 15) {
+                        good = false;
+                    } else {
+                        uint32_t b;
+                        int32_t run = 0;
+                        do {
+                            b = PB(q);
+                            ++q;
+                            lit += b;
+                            if (q > iend - 15) good = false;
+                            // a run past kPRunCap bytes (a literal of >= 4 KiB: an
+                            // incompressible block's single literal is ~257) goes to
+                            // the finisher: not read byte by byte here, mostly from HBM
+                            if (++run >= kPRunCap && b == 255) good = false;
+                        } while (good && b == 255);
+                        if (good && (op + lit > oend - 32 || q + lit > iend - 32)) good = false;   // :2016-2027
+                    }
+                } else if (q > iend - 17) {   // :2034
+                    good = false;
+                }
+                if (good) {
+                    const int32_t po = q + (int32_t)lit;
+                    const uint32_t off = PB(po) | (PB(po + 1) << 8);
+                    pe = po + 2;
+                    ml = tok & 15;
+                    if (ml == 15) {   // read_variable_length(&ip, iend - 4, 0)
+                        uint32_t b;
+                        int32_t run = 0;
+                        do {
+                            b = PB(pe);
+                            ++pe;
+                            ml += b;
+                            if (pe > iend - 4) good = false;
+                            if (++run >= kPRunCap && b == 255) good = false;   // (as above)
+                        } while (good && b == 255);
+                    }
+                    ml += 4;
+                    // offset 0 and offsets before the block start go to the exact
+                    // path (lz4.c:2071, :2081); so do matches reaching oend - 64 (:2073, :2076)
+                    if (good && (off == 0 || (int64_t)off > (int64_t)op + lit || (int64_t)op + lit + ml >= (int64_t)oend - 64))
+                        good = false;
+                }
 #undef PB
+            }
             if (good) {
                 const int32_t adv = pe - ip;
                 stg[k & (kPStage - 1)] = (uint8_t)(adv < 255 ? adv : 255);
@@ -559,6 +625,44 @@ __global__ __launch_bounds__(kPWG) void rows_parse_kernel(const uint8_t* __restr
         // ---- the common sequence, straight-line, until too few lanes can go on
         RP_MARK(1);
         const int32_t thr = min(LZ4M_PARSE_MIN_ACTIVE, (int)__popcll(__ballot(live)));
+#if LZ4M_PARSE_V2
+        // two steps per count of the lanes that can go on; every lane runs
+        // both (predicated, no exec-mask branches): a lane that cannot take
+        // its sequence stops (`stall`) -- at its ring's end or a full length
+        // ring until the next general step rotates or flushes, or for a
+        // sequence the fast test does not cover (`need`: the general parse)
+        while (true) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const bool go = live && !need && !stall;
+                RP_COUNT(3, u == 0);
+                RP_COUNT(5, u == 0 ? __popcll(__ballot(go)) : 0);
+                const bool inw = ip + 16 <= wb + kPW;
+                const bool room = k - kf < kPStage - 1;
+                const u32x4 w = ring_ld16(W, ip & (kPW - 1));
+                const int32_t tok = (int32_t)(w.x & 0xFFu), lit = tok >> 4, mlc = tok & 15;
+                const bool mlx = mlc == 15;
+                const uint32_t dw = dword_at(w, (uint32_t)(1 + lit));   // offset, then the match-length byte
+                const int32_t off = (int32_t)(dw & 0xFFFFu);
+                const int32_t ext = (int32_t)((dw >> 16) & 0xFFu);
+                const int32_t adv = 3 + lit + (int32_t)mlx;
+                const int32_t ml = mlc + 4 + (mlx ? ext : 0);
+                const bool fast = (lit <= 12) & !(mlx & (ext == 255)) & (ip + 1 <= iend - 17) &
+                                  (!mlx | (ip + adv <= iend - 4)) & (off != 0) & (off <= op + lit) &
+                                  (op + lit + ml < oend - 64);
+                const bool take = go & inw & room & fast;
+                // slot k is free (one slot of the ring always is): written even
+                // when the sequence is not taken, then overwritten
+                stg[k & (kPStage - 1)] = (uint8_t)adv;
+                ip += take ? adv : 0;
+                op += take ? lit + ml : 0;
+                k += (int32_t)take;
+                stall = stall | (go & !take);
+                need = need | (go & inw & room & !fast);
+            }
+            if ((int)__popcll(__ballot(live && !need && !stall)) < max(thr, 1)) break;
+        }
+#else
         while (true) {
             const bool go = live && !need;
             if ((int)__popcll(__ballot(go)) < max(thr, 1)) break;
@@ -568,9 +672,6 @@ __global__ __launch_bounds__(kPWG) void rows_parse_kernel(const uint8_t* __restr
                 // straight-line: no short-circuit tests
                 const bool inw = ip + 16 <= wb + kPW;
                 const u32x4 w = ring_ld16(W, ip & (kPW - 1));
-#if LZ4M_PARSE_PAIR
-                const u32x4 w2 = ring_ld16(W, (ip + 16) & (kPW - 1));   // the next 16 ring bytes
-#endif
                 const int32_t tok = (int32_t)(w.x & 0xFFu), lit = tok >> 4, mlc = tok & 15;
                 const bool mlx = mlc == 15;
                 const uint32_t dw = dword_at(w, (uint32_t)(1 + lit));   // offset, then the match-length byte
@@ -584,40 +685,13 @@ __global__ __launch_bounds__(kPWG) void rows_parse_kernel(const uint8_t* __restr
                 // slot k is free (one slot of the ring always is): written even
                 // when the sequence is not taken, then overwritten
                 stg[k & (kPStage - 1)] = (uint8_t)adv;
-#if LZ4M_PARSE_PAIR
-                // the sequence after it, from the same 32 ring bytes: it
-                // starts at byte adv (<= 16 for a taken sequence) of w|w2
-                const int32_t ip2 = ip + adv, op2 = op + lit + ml;
-                const uint32_t a2 = (uint32_t)adv & 31u;
-                const uint32_t t2 = dword32(w, w2, a2 > 28u ? 28u : a2) >> (8u * (a2 > 28u ? a2 - 28u : 0u));
-                const int32_t tok2 = (int32_t)(t2 & 0xFFu), lit2 = tok2 >> 4, mlc2 = tok2 & 15;
-                const bool mlx2 = mlc2 == 15;
-                const uint32_t p2 = a2 + 1u + (uint32_t)lit2;   // offset, then the match-length byte
-                const uint32_t dw2 = dword32(w, w2, p2 > 28u ? 28u : p2) >> (8u * (p2 > 28u ? p2 - 28u : 0u));
-                const int32_t off2 = (int32_t)(dw2 & 0xFFFFu);
-                const int32_t ext2 = (int32_t)((dw2 >> 16) & 0xFFu);
-                const int32_t adv2 = 3 + lit2 + (int32_t)mlx2;
-                const int32_t ml2 = mlc2 + 4 + (mlx2 ? ext2 : 0);
-                // the same tests as the first; all its bytes lie in w|w2
-                // (p2 + 3 <= 31) and inside the ring
-                const bool ok2 = ok & (p2 + 3u <= 31u) & (ip2 + 16 <= wb + kPW) & (lit2 <= 12) &
-                                 !(mlx2 & (ext2 == 255)) & (ip2 + 1 <= iend - 17) & (!mlx2 | (ip2 + adv2 <= iend - 4)) &
-                                 (off2 != 0) & (off2 <= op2 + lit2) & (op2 + lit2 + ml2 < oend - 64) &
-                                 (k + 1 - kf < kPStage - 1);
-                // slot k + 1 is free when the first is taken (then k - kf <= 30);
-                // otherwise slot k is, and nothing is taken
-                stg[(ok ? k + 1 : k) & (kPStage - 1)] = (uint8_t)adv2;
-                ip += (ok ? adv : 0) + (ok2 ? adv2 : 0);
-                op += (ok ? lit + ml : 0) + (ok2 ? lit2 + ml2 : 0);
-                k += (int32_t)ok + (int32_t)ok2;
-#else
                 ip += ok ? adv : 0;
                 op += ok ? lit + ml : 0;
                 k += (int32_t)ok;
-#endif
                 need = !ok;
             }
         }
+#endif
     }
     RP_FLUSH(0, 8);
 }
@@ -1168,8 +1242,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LZ4M_ROWS_WA
             pend = pend && !ready;
         }
 #endif
-        if (LZ4M_ROWS_ORDER) parse_ahead();
         RP_MARK(13);
+        if (LZ4M_ROWS_ORDER) parse_ahead();
+        RP_MARK(15);
         // ---- flush, advance, rebase for the next round
         const int32_t opn = P.opn;
 #if LZ4M_ROWS_COUNTED

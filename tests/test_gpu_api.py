@@ -737,6 +737,66 @@ def test_single_call_many_threads(gpu, oracle):
     assert N.lib().lz4m_single_call_worker_state(st) == 0   # no worker missed its 1 s deadline (none turned off)
 
 
+def test_batched_launch_beside_single_call_loop(gpu):
+    """A batched decode on torch's current stream while another host thread
+    loops lz4.block.compress through its persistent worker (a
+    stream that shares the worker's hardware queue waits behind it).  The
+    worker ends every launch after at most 5 ms (kLife) and 2 ms idle
+    (kIdle), so a batched launch waits at most a few milliseconds whatever
+    the call rate; the measured cost is printed."""
+    import threading
+    import time
+    import torch
+    import lz4._native as N
+    import lz4.block
+    n = 8192
+    rng = np.random.default_rng(3)
+    plain = rng.integers(0, 256, (n, 4096), dtype=np.uint8)
+    plain[:, ::3] = 7                                   # compressible
+    comp = lz4.block.compress_many([bytes(r) for r in plain], store_size=False)
+    packed = torch.frombuffer(bytearray(b"".join(comp)), dtype=torch.uint8).to(gpu)
+    lens = torch.tensor([len(c) for c in comp], dtype=torch.int32, device=gpu)
+    offs = torch.cumsum(lens.to(torch.int64), 0) - lens.to(torch.int64)
+    dst = torch.empty(n * 4096, dtype=torch.uint8, device=gpu)
+    doff = torch.arange(n, dtype=torch.int64, device=gpu) * 4096
+    dcap = torch.full((n,), 4096, dtype=torch.int32, device=gpu)
+    st = torch.empty(n, dtype=torch.int32, device=gpu)
+
+    def timed(reps=20):
+        ts = []
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            N.launch_decompress(packed, offs, lens, dst, doff, dcap, st, n)
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        return sorted(ts)[len(ts) // 2], max(ts)
+
+    timed(3)
+    alone = timed()
+    stop = threading.Event()
+    block = rng.integers(0, 256, 65536, dtype=np.uint8).tobytes()
+    calls = [0]
+
+    def loop():
+        while not stop.is_set():
+            lz4.block.compress(block)
+            calls[0] += 1
+
+    th = threading.Thread(target=loop)
+    th.start()
+    try:
+        time.sleep(0.05)
+        beside = timed()
+    finally:
+        stop.set()
+        th.join(timeout=60)
+    assert bool((st == 4096).all()) and torch.equal(dst.view(n, 4096).cpu(), torch.from_numpy(plain))
+    print(f"batched decode of {n} blocks: median/max {alone[0] * 1e3:.2f}/{alone[1] * 1e3:.2f} ms alone, "
+          f"{beside[0] * 1e3:.2f}/{beside[1] * 1e3:.2f} ms beside {calls[0]} single calls")
+    assert beside[1] < alone[1] + 0.05, (alone, beside)   # bounded by the worker's 5 ms lifetime, not unbounded
+
+
 @pytest.mark.parametrize("size", [(40 << 20) + 12345, (96 << 20) + 7])
 def test_frame_dropin_large_odd_sizes(gpu, reference, size):
     """lz4.frame.compress / decompress on host bytes large enough for the

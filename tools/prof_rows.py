@@ -16,8 +16,8 @@ from lz4 import _native as N  # noqa: E402
 dev = torch.device("cuda", 0)
 lib = N.lib()
 PN = {0: "assign", 1: "general step", 2: "fast loop"}
-EN = {14: "block grab", 8: "sync parse", 10: "use==0 paths", 11: "parse ahead", 12: "literal",
-      13: "passes", 9: "flush+rebase", 20: "block end flush", 21: "non-fit copy", 22: "nseq0 skip"}
+EN = {14: "block grab", 8: "sync parse", 10: "use==0 paths", 11: "literal", 12: "pass setup",
+      13: "passes", 15: "parse ahead", 9: "flush+rebase", 20: "block end flush", 21: "non-fit copy", 22: "nseq0 skip"}
 for kind in os.environ.get("KINDS", "silesia").split(","):
     nb = int(os.environ.get("NB", "262144"))
     src = B.make_batch(nb, min(4096, nb), kind, 7, dev)
