@@ -156,12 +156,20 @@ __device__ __forceinline__ void wave_copy(uint8_t* d, const uint8_t* s, int64_t 
     }
 }
 
+// LZ4M_COMPRESS_XP (timing probes only, WRONG output): bit 1 = the parse
+// issues no store of its output (compress_block_w), to measure what the
+// stores' place in the in-order memory counter costs the serial parse
+#ifndef LZ4M_COMPRESS_XP
+#define LZ4M_COMPRESS_XP 0
+#endif
+#define CST(stmt) do { if (!(LZ4M_COMPRESS_XP & 1)) { stmt; } } while (0)
+
 // length bytes after a token nibble of 15 (lz4.c:1094-1099, 1184-1194);
 // returns the new output position.  Written by lane 0.
 __device__ __forceinline__ int64_t put_len(uint8_t* dst, int64_t op, int64_t len, uint32_t lane) {
     const int64_t n255 = len / 255;
-    for (int64_t k = lane; k < n255; k += kWave) dst[op + k] = 255;
-    if (lane == 0) dst[op + n255] = (uint8_t)(len - 255 * n255);
+    for (int64_t k = lane; k < n255; k += kWave) CST(dst[op + k] = 255);
+    if (lane == 0) CST(dst[op + n255] = (uint8_t)(len - 255 * n255));
     return op + n255 + 1;
 }
 
@@ -584,9 +592,9 @@ __device__ __forceinline__ int32_t compress_block_w(const uint8_t* __restrict__ 
                         }
                     }
                     if (lit - q >= 16 || d_room - q >= 16) {
-                        st16(d + q, v);
+                        CST(st16(d + q, v));
                     } else {
-                        for (int32_t j = 0; j < lit - q; ++j) d[q + j] = (uint8_t)byte_of(v, (int)j);
+                        for (int32_t j = 0; j < lit - q; ++j) CST(d[q + j] = (uint8_t)byte_of(v, (int)j));
                     }
                 }
             }
@@ -598,8 +606,8 @@ __device__ __forceinline__ int32_t compress_block_w(const uint8_t* __restrict__ 
         {   // ---- offset + match length (lz4.c:1125-1197) ----
             const uint32_t off = (uint32_t)(ip - match);
             if (lane == 0) {
-                dst[op] = (uint8_t)off;
-                dst[op + 1] = (uint8_t)(off >> 8);
+                CST(dst[op] = (uint8_t)off);
+                CST(dst[op + 1] = (uint8_t)(off >> 8));
             }
             op += 2;
             // LZ4_count(ip+4, match+4, matchlimit): bytes 4..15 of P/G first,
@@ -661,7 +669,7 @@ __device__ __forceinline__ int32_t compress_block_w(const uint8_t* __restrict__ 
             } else {
                 tok_lo = (uint32_t)mcode;
             }
-            if (lane == 0) dst[tok_pos] = (uint8_t)(tok_hi + tok_lo);
+            if (lane == 0) CST(dst[tok_pos] = (uint8_t)(tok_hi + tok_lo));
             CP_MARK(5);
         }
         anchor = ip;

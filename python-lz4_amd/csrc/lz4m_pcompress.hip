@@ -310,6 +310,9 @@ __device__ __forceinline__ uint64_t chunk_finish(const Chunk& C, int32_t p0, int
     return __ballot(ok);
 }
 
+#ifndef LZ4M_PC_ORDER
+#define LZ4M_PC_ORDER 0
+#endif
 template <bool BIG, int HB>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BIG || HB > 12 ? 1 : 5))) void pcompress_kernel(const uint8_t* __restrict__ src,
                                                        const int64_t* __restrict__ src_off,
@@ -354,10 +357,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BIG || HB > 
             const bool has_next = p0 + 68 <= N;
             Chunk B;
             uint32_t wafter = 0;
-            if (has_next) {
-                chunk_issue<BIG, HB>(B, s, table, p0 + 64, wnext, N, mlast, lane);
-                if (p0 + 132 <= N) wafter = load_word(s, p0 + 128 + (int32_t)lane, N);
-            }
+            // LZ4M_PC_ORDER 1: B's loads are issued after A's walk, whose
+            // long-match counts and catch-up loads wait at once (gfx9 counts
+            // loads in order: such a wait would also wait for B's)
+            auto issue_b = [&]() __attribute__((always_inline)) {
+                if (has_next) {
+                    chunk_issue<BIG, HB>(B, s, table, p0 + 64, wnext, N, mlast, lane);
+                    if (p0 + 132 <= N) wafter = load_word(s, p0 + 128 + (int32_t)lane, N);
+                }
+            };
+            if (!LZ4M_PC_ORDER) issue_b();
             // ---- greedy parse of chunk p0.  The serial walk only picks the
             // sequence starts: the first verified lane at or after the previous
             // match's end (catch-up moves a start back but not the end).
@@ -430,9 +439,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BIG || HB > 
                 q_pb = __builtin_amdgcn_ds_permute(addr, ipsz - psz);
                 anchor = cur;
             }
+            if (LZ4M_PC_ORDER) issue_b();
             int32_t LB = 0, backB = 0;
             uint64_t maskB = 0;
-            if (has_next) maskB = chunk_finish(B, p0 + 64, matchlimit, LB, backB, lane);
+            if (!LZ4M_PC_ORDER && has_next) maskB = chunk_finish(B, p0 + 64, matchlimit, LB, backB, lane);
             if (ns > 0) {
                 const int32_t w = emit_seqs<BIG>(s, d, op, cap, ns, q_ls, q_lit, q_off, q_ml, q_ob, q_pb, acc, pacc, p0,
                                             A.v, vprev, lane);
@@ -442,6 +452,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BIG || HB > 
                 }
                 op += w;
             }
+            if (LZ4M_PC_ORDER && has_next) maskB = chunk_finish(B, p0 + 64, matchlimit, LB, backB, lane);
             if (!has_next) break;
             vprev = A.v;
             A.v = B.v;

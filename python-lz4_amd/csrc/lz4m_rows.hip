@@ -933,35 +933,44 @@ __device__ __forceinline__ int32_t load_len(const uint8_t* dl, int32_t k, int32_
 #ifndef LZ4M_ROWS_WAVES
 #define LZ4M_ROWS_WAVES 5   // waves per SIMD the executor's registers are held to (LDS allows 5)
 #endif
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LZ4M_ROWS_WAVES, 8))) void rows_exec_kernel(const uint8_t* __restrict__ src,
+// LZ4M_ROWS_EWG: threads per workgroup (64 or 256).  The waves of a
+// workgroup are independent (no barrier after the prologue); 256 shares the
+// put-mask and period tables (1.6 KB of LDS) between four waves.
+#ifndef LZ4M_ROWS_EWG
+#define LZ4M_ROWS_EWG 64
+#endif
+constexpr int kEWG = LZ4M_ROWS_EWG;
+static_assert(kEWG == 64 || kEWG == 256, "executor workgroup: 64 or 256 threads");
+__global__ __launch_bounds__(kEWG) __attribute__((amdgpu_waves_per_eu(LZ4M_ROWS_WAVES, 8))) void rows_exec_kernel(const uint8_t* __restrict__ src,
                                                        const int64_t* __restrict__ src_off,
                                                        const int32_t* __restrict__ src_len, uint8_t* dst,
                                                        const int64_t* __restrict__ dst_off,
                                                        const RowMeta* __restrict__ meta,
                                                        const uint8_t* __restrict__ lens, int64_t n,
                                                        unsigned long long* __restrict__ ctr) {
-    __shared__ __attribute__((aligned(16))) uint8_t hists[4 * kRowsHS];
+    __shared__ __attribute__((aligned(16))) uint8_t hists[kEWG / 16 * kRowsHS];
 #if LZ4M_LDS_ALIGN
     __shared__ __attribute__((aligned(16))) uint32_t mtab[kPutTab];
 #else
-    __shared__ __attribute__((aligned(16))) uint8_t dums[64 * 16];
+    __shared__ __attribute__((aligned(16))) uint8_t dums[kEWG * 16];
 #endif
     __shared__ __attribute__((aligned(16))) uint32_t psel[16 * 8];
-    __shared__ __attribute__((aligned(16))) u32x4 xsl[64 * 2];
-    const uint32_t lane = threadIdx.x;
+    __shared__ __attribute__((aligned(16))) u32x4 xsl[kEWG * 2];
+    const uint32_t lane = threadIdx.x & 63u;   // lane of the wave
     const int32_t jj = (int32_t)(lane & 15), r = (int32_t)(lane >> 4);
-    lds_u8* HB = (lds_u8*)(hists + r * kRowsHS);
+    lds_u8* HB = (lds_u8*)(hists + (threadIdx.x >> 4) * kRowsHS);   // the row's history
 #if LZ4M_LDS_ALIGN
-    lds_put_table_init(mtab, lane, 64);
+    lds_put_table_init(mtab, threadIdx.x, kEWG);
     lds_cu32* MT = (lds_cu32*)mtab;
 #else
-    lds_u8* DUM = (lds_u8*)(dums + lane * 16);
+    lds_u8* DUM = (lds_u8*)(dums + threadIdx.x * 16);
 #endif
-    period_sel_init(psel, lane, 64);
+    period_sel_init(psel, threadIdx.x, kEWG);
+    if (kEWG > 64) __syncthreads();   // tables written by other waves
     lds_cu32* PS = (lds_cu32*)psel;
-    lds_u32x4* XSL = (lds_u32x4*)(xsl + 2 * lane);
+    lds_u32x4* XSL = (lds_u32x4*)(xsl + 2 * threadIdx.x);
     // this lane's dummy store target (flush stores of lanes with nothing final)
-    uint8_t* const dst_dummy = reinterpret_cast<uint8_t*>(ctr) + kRowsDummy + 1024 * (blockIdx.x % kRowsDummySlots) + 16 * lane;
+    uint8_t* const dst_dummy = reinterpret_cast<uint8_t*>(ctr) + kRowsDummy + 1024 * ((blockIdx.x * (kEWG / 64) + (threadIdx.x >> 6)) % kRowsDummySlots) + 16 * lane;
     (void)dst_dummy;
     // row state (uniform across the row's 16 lanes)
     const uint8_t* s = nullptr;
@@ -1322,7 +1331,7 @@ extern "C" int lz4m_rows_launch(const uint8_t* d_src, const int64_t* d_src_off, 
     if (e != hipSuccess) return (int)e;
     hipLaunchKernelGGL(rows_parse_kernel, dim3((uint32_t)parse_grid), dim3(kPWG), 0, stream, d_src, d_src_off,
                        d_src_len, d_dst_cap, n, meta, lens, lens_cap, ctr);
-    hipLaunchKernelGGL(rows_exec_kernel, dim3((uint32_t)exec_grid), dim3(64), 0, stream, d_src, d_src_off, d_src_len,
+    hipLaunchKernelGGL(rows_exec_kernel, dim3((uint32_t)exec_grid), dim3(kEWG), 0, stream, d_src, d_src_off, d_src_len,
                        d_dst, d_dst_off, meta, lens, n, ctr);
     return (int)hipGetLastError();
 }
@@ -1332,10 +1341,10 @@ extern "C" int lz4m_rows_grids(int64_t n, int* parse_grid, int* exec_grid) {
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&pk, reinterpret_cast<const void*>(rows_parse_kernel), kPWG, 0);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&ek, reinterpret_cast<const void*>(rows_exec_kernel), 64, 0);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&ek, reinterpret_cast<const void*>(rows_exec_kernel), kEWG, 0);
     if (cus <= 0) cus = 256;
     const int64_t ps = (int64_t)cus * (pk > 0 ? pk : 1), es = (int64_t)cus * (ek > 0 ? ek : 1);
-    const int64_t pneed = (n + kPWG - 1) / kPWG, eneed = (n + 3) / 4;
+    const int64_t pneed = (n + kPWG - 1) / kPWG, eneed = (n + kEWG / 16 - 1) / (kEWG / 16);
     *parse_grid = (int)(pneed < ps ? pneed : ps);
     *exec_grid = (int)(eneed < es ? eneed : es);
     return 0;

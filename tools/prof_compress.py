@@ -35,15 +35,17 @@ for kind in kinds:
             torch.cuda.synchronize()
             ts.append(a.elapsed_time(b))
         tot = int(olen.to(torch.int64).sum())
-        assert int((olen <= 0).sum()) == 0
+        nocheck = os.environ.get("NOCHECK") == "1"   # timing probes whose output is wrong on purpose
+        assert nocheck or int((olen <= 0).sum()) == 0
         # round trip through the GPU decoder
         dst = torch.empty(n * 65536, dtype=torch.uint8, device=dev)
         doff = torch.arange(n, dtype=torch.int64, device=dev) * 65536
         dcap = torch.full((n,), 65536, dtype=torch.int32, device=dev)
         st = torch.empty(n, dtype=torch.int32, device=dev)
-        N.launch_decompress(slots, soff, olen, dst, doff, dcap, st, n)
-        torch.cuda.synchronize()
-        assert torch.equal(dst, src), (kind, mode)
+        if not nocheck:
+            N.launch_decompress(slots, soff, olen, dst, doff, dcap, st, n)
+            torch.cuda.synchronize()
+            assert torch.equal(dst, src), (kind, mode)
         del dst
         ms = min(ts)
         row[mode] = {"ms": round(ms, 2), "GiB_s": round(n * 65536 / ms / 1e-3 / 2**30, 2), "bytes": tot,
