@@ -373,7 +373,7 @@ uint32_t lz4m_xxh32_host(const void* input, size_t length, uint32_t seed);
  * on blocks up to 64 KiB) are served by a persistent one-workgroup kernel per
  * host thread and kind that polls a mailbox in mapped pinned memory, so a
  * call while others keep coming pays no kernel launch; it exits after 2 ms
- * without a call or 1 ms after it started (whatever the call rate: work on a
+ * without a call or 2 ms after it started (whatever the call rate: work on a
  * stream that shares its hardware queue waits at most that long) and is
  * started again by the next call.  mode 1 = on (the
  * default; env LZ4M_WORKER=0 turns it off), 0 = off (one launch of the

@@ -163,6 +163,16 @@ __device__ __forceinline__ void wave_copy(uint8_t* d, const uint8_t* s, int64_t 
 #define LZ4M_COMPRESS_XP 0
 #endif
 #define CST(stmt) do { if (!(LZ4M_COMPRESS_XP & 1)) { stmt; } } while (0)
+// LZ4M_CMP_TNMERGE: at acceleration 1 the test of the next position after a
+// match (lz4.c:1207-1258) is lane 0 of the next search step instead of a
+// step of its own.  Exact: it is the search attempt at ip with anchor == ip
+// (no catch-up, no literals), after the insert of ip - 2; the step's other
+// lanes are the first 63 attempts of the search from ip + 1 that follows a
+// failed test (the output-limit check of a zero-length literal run is implied
+// by the match's, lz4.c:1085-1089 vs 1184-1190).
+#ifndef LZ4M_CMP_TNMERGE
+#define LZ4M_CMP_TNMERGE 1
+#endif
 
 // length bytes after a token nibble of 15 (lz4.c:1094-1099, 1184-1194);
 // returns the new output position.  Written by lane 0.
@@ -422,6 +432,7 @@ __device__ __forceinline__ int32_t compress_block_w(const uint8_t* __restrict__ 
     int32_t pbase = 0, gbase = 0, back = 0;
 
     int32_t staged = 0;   // LW with `stage`: bytes known to be in LDS (wave uniform)
+    int32_t tnb = 0;      // 1: the next search step starts with the test of position ip (LZ4M_CMP_TNMERGE)
     CP_DECL
     if (n < kMinLength) goto last_literals;                    // lz4.c:981
 
@@ -437,12 +448,16 @@ __device__ __forceinline__ int32_t compress_block_w(const uint8_t* __restrict__ 
         uint32_t PM, GM;
         {   // ---- search (lz4.c:1016-1075), 64 attempts per wave step ----
             SI k0 = 0;
+            // the search origin (lz4.c:1017 forwardIp): ip, or ip + 1 after the
+            // test of ip in lane 0 (tnb); attempt k of lane l: k = k0 + l - tnb
+            const int32_t ipo = ip + tnb;
             for (;;) {
-                const SI k = k0 + (SI)lane;
+                const SI k = k0 + (SI)lane - (SI)tnb;
                 // attempts 0..63 of acceleration 1 are consecutive positions
+                // (with tnb, lane 0's "attempt -1" is the tested position ip)
                 const bool unit = A == 64 && k0 == 0;
-                const SI pos64 = ip + (unit ? k : attempt_off<SI>(k, A, FA));
-                const SI nxt = unit ? pos64 + 1 : ip + 1 + skip_sum<SI>(A + k - 1) - FA;   // attempt k+1
+                const SI pos64 = ipo + (unit ? k : attempt_off<SI>(k, A, FA));
+                const SI nxt = unit ? pos64 + 1 : ipo + 1 + skip_sum<SI>(A + k - 1) - FA;   // attempt k+1
                 const bool valid = nxt <= (SI)mflimit1;
                 const int32_t pos = valid ? (int32_t)pos64 : ip;
                 const uint64_t vmask = __ballot(valid);
@@ -468,6 +483,11 @@ __device__ __forceinline__ int32_t compress_block_w(const uint8_t* __restrict__ 
                 // does not read its own id back shares its hash with another
                 // lane of this step (one LDS round trip, in order per wave)
                 uint32_t h = 0, old = 0, rb = lane;
+                if (tnb && k0 == 0 && lane == 0) {   // lz4.c:1207-1208: ip - 2 first
+                    const u32x4 pv2 = u32x4{__builtin_amdgcn_alignbyte(pv.x, pm, 2),
+                                            __builtin_amdgcn_alignbyte(pv.y, pv.x, 2), 0u, 0u};
+                    T::put_v(tab, T::hash_v(pv2), cur - 2u);
+                }
                 if (valid) {
                     h = T::hash_v(pv);
                     old = T::get_v(tab, h);
@@ -495,7 +515,9 @@ __device__ __forceinline__ int32_t compress_block_w(const uint8_t* __restrict__ 
                 CP_MARK(1);
                 // the serial loop inserted an earlier lane of the group first
                 const uint32_t cand =
-                    pred >= 0 ? ibase + (uint32_t)(ip + (unit ? (SI)pred : attempt_off<SI>(k0 + pred, A, FA))) : old;
+                    pred >= 0 ? ibase + (uint32_t)(ipo + (unit ? (SI)pred - (SI)tnb
+                                                               : attempt_off<SI>(k0 + (SI)pred - (SI)tnb, A, FA)))
+                              : old;
                 int32_t cpos = pos;
                 bool ok = false;
                 u32x4 gv = u32x4{0, 0, 0, 0};
@@ -674,6 +696,10 @@ __device__ __forceinline__ int32_t compress_block_w(const uint8_t* __restrict__ 
         }
         anchor = ip;
         if (ip >= mflimit1) break;                             // lz4.c:1204
+        if (LZ4M_CMP_TNMERGE && A == 64) {   // the test of ip: lane 0 of the next search step
+            tnb = 1;
+            continue;
+        }
 
         {   // ---- fill table, test next position (lz4.c:1207-1258) ----
             uint32_t pm;

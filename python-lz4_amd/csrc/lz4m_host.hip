@@ -171,7 +171,7 @@ constexpr size_t kWorkOut = 1 << 20;          // output region: capacities up to
 constexpr size_t kWorkMb = 128;               // two mailboxes
 constexpr uint64_t kIdle = 200000;            // 2 ms of the 100 MHz real-time clock
 #ifndef LZ4M_WORKER_LIFE
-#define LZ4M_WORKER_LIFE 100000               // 1 ms of the 100 MHz clock: a launch's whole lifetime
+#define LZ4M_WORKER_LIFE 200000               // 2 ms of the 100 MHz clock: a launch's whole lifetime
 #endif
 constexpr uint64_t kLife = LZ4M_WORKER_LIFE;
 constexpr int32_t kSoloStageFail = -2;        // lone-block compress: a staging wait gave up (lz4m_compress.hip)

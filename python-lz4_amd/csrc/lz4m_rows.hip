@@ -719,6 +719,9 @@ constexpr int32_t kRowsH = LZ4M_ROWS_H;
 #define LZ4M_ROWS_ORDER 1   // 1 (required: FarSrc is shared by P and Q): parse ahead after this round's passes
 #endif
 static_assert(LZ4M_ROWS_ORDER == 1, "the far-source pieces (FarSrc) are reused by the round parsed ahead");
+#ifndef LZ4M_ROWS_ENDS
+#define LZ4M_ROWS_ENDS 1    // a round whose rows all take 16 sequences: next (ip, op) = lane 15's ends (no scans)
+#endif
 #ifndef LZ4M_ROWS_XP
 #define LZ4M_ROWS_XP 0      // timing probes, WRONG output (r05a): 2 no HBM loads in passes, 4 no late loads, 8 no far prefetch
 #endif
@@ -841,11 +844,17 @@ __device__ __forceinline__ void parse_round(PSeq& P, int32_t jj, int32_t r, int3
     const int32_t o = op + row_incl_sum(len) - len;
     const int32_t mend = o + lit + ml;
     const bool ok = act & !esc & (mend <= bnext + kRowsH);
-    const uint32_t rb = (uint32_t)(__ballot(!ok) >> (16 * r)) & 0xFFFFu;
+    const uint64_t nok = __ballot(!ok);
+    const uint32_t rb = (uint32_t)(nok >> (16 * r)) & 0xFFFFu;
     const int32_t use = rb ? __builtin_ctz(rb) : 16;
     const bool u = jj < use;
-    P.opn = op + row_last(row_incl_sum(u ? len : 0));
-    P.ipn = ip + row_last(row_incl_sum(u ? dlt : 0));
+    if (LZ4M_ROWS_ENDS && nok == 0) {   // every row takes its 16 sequences: the ends of lane 15's
+        P.opn = row_last(o + len);
+        P.ipn = row_last(t + dlt);
+    } else {
+        P.opn = op + row_last(row_incl_sum(u ? len : 0));
+        P.ipn = ip + row_last(row_incl_sum(u ? dlt : 0));
+    }
     const int32_t s0 = o + lit - off;
     const bool far = u & (s0 < bnext);
     const bool late = far & (s0 + 32 > F);

@@ -73,6 +73,26 @@ __global__ __launch_bounds__(64) void k(uint32_t seed, uint32_t* out, unsigned l
 #define X(i) asm volatile("v_add_u32 %0, %0, %1\n v_and_b32 %0, %0, %1" : "+v"(a##i) : "v"(c));
             REP4(X(0) X(1) X(2) X(3))
 #undef X
+        } else if (OP == 14) {   // the select form the compiler emits: VOP3 with an SGPR-pair mask
+#define X(i) asm volatile("v_cndmask_b32_e64 %0, %0, %1, s[10:11]" : "+v"(a##i) : "v"(c) : "s10", "s11");
+            REP4(R8(X))
+#undef X
+        } else if (OP == 15) {   // v_add_u32 in its VOP3 encoding
+#define X(i) asm volatile("v_add_u32_e64 %0, %0, %1" : "+v"(a##i) : "v"(c));
+            REP4(R8(X))
+#undef X
+        } else if (OP == 16) {
+#define X(i) asm volatile("v_or3_b32 %0, %0, %1, %1" : "+v"(a##i) : "v"(c));
+            REP4(R8(X))
+#undef X
+        } else if (OP == 17) {   // compare to an SGPR pair, then select on it (pairs)
+#define X(i) asm volatile("v_cmp_gt_i32_e64 s[12:13], %0, %1\n v_cndmask_b32_e64 %0, %0, %1, s[12:13]" : "+v"(a##i) : "v"(c) : "s12", "s13");
+            REP4(X(0) X(1) X(2) X(3))
+#undef X
+        } else if (OP == 18) {   // v_and_b32 (VOP2)
+#define X(i) asm volatile("v_and_b32 %0, %0, %1" : "+v"(a##i) : "v"(c));
+            REP4(R8(X))
+#undef X
         } else if (OP == 13) {   // ds_read-free scalar op mix: s_add per 2 VALU (SALU co-issue)
 #define X(i) asm volatile("v_add_u32 %0, %0, %1\n s_add_u32 s40, s40, 1" : "+v"(a##i) : "v"(c) : "s40", "scc");
             REP4(R8(X))
@@ -117,7 +137,7 @@ int main() {
     hipMalloc(&out, sizeof(uint32_t) * 256 * 4 * 8 * 64);
     hipMalloc(&span, sizeof(unsigned long long) * 256 * 4 * 8);
     static unsigned long long hspan[256 * 4 * 8];
-    for (int w : {1, 2, 5, 8}) {
+    for (int w : {2, 5, 8}) {
         run<0>("v_add_u32", w, out, span, hspan);
         run<1>("v_perm_b32", w, out, span, hspan);
         run<2>("v_alignbyte_b32", w, out, span, hspan);
@@ -132,6 +152,11 @@ int main() {
         run<11>("v_add_co_u32", w, out, span, hspan);
         run<12>("add+and", w, out, span, hspan);
         run<13>("add + s_add", w, out, span, hspan);
+        run<14>("v_cndmask_b32_e64 sgpr", w, out, span, hspan);
+        run<15>("v_add_u32_e64", w, out, span, hspan);
+        run<16>("v_or3_b32", w, out, span, hspan);
+        run<17>("v_cmp_e64 + v_cndmask", w, out, span, hspan);
+        run<18>("v_and_b32", w, out, span, hspan);
     }
     hipFree(out);
     hipFree(span);
