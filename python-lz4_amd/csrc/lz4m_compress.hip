@@ -156,6 +156,15 @@ __device__ __forceinline__ void wave_copy(uint8_t* d, const uint8_t* s, int64_t 
     }
 }
 
+// Exactly k bytes (k >= 16: 16) of v at global address p
+__device__ __forceinline__ void gbl_put_c(uint8_t* p, u32x4 v, int32_t k) {
+    if (k >= 16) {
+        st16(p, v);
+        return;
+    }
+    for (int32_t j = 0; j < k; ++j) p[j] = (uint8_t)byte_of(v, j);
+}
+
 // LZ4M_COMPRESS_XP (timing probes only, WRONG output): bit 1 = the parse
 // issues no store of its output (compress_block_w), to measure what the
 // stores' place in the in-order memory counter costs the serial parse
@@ -164,14 +173,20 @@ __device__ __forceinline__ void wave_copy(uint8_t* d, const uint8_t* s, int64_t 
 #endif
 #define CST(stmt) do { if (!(LZ4M_COMPRESS_XP & 1)) { stmt; } } while (0)
 // LZ4M_CMP_TNMERGE: at acceleration 1 the test of the next position after a
-// match (lz4.c:1207-1258) is lane 0 of the next search step instead of a
+// match (lz4.c:1207-1258) may be lane 0 of the next search step instead of a
 // step of its own.  Exact: it is the search attempt at ip with anchor == ip
 // (no catch-up, no literals), after the insert of ip - 2; the step's other
 // lanes are the first 63 attempts of the search from ip + 1 that follows a
 // failed test (the output-limit check of a zero-length literal run is implied
-// by the match's, lz4.c:1085-1089 vs 1184-1190).
+// by the match's, lz4.c:1085-1089 vs 1184-1190).  A 64-lane step costs more
+// than the lone test, so this pays only where the test mostly fails: the
+// parse keeps a running hit rate of the test (1/256 units, weight 1/8) and
+// merges while it is below LZ4M_CMP_TNMERGE (0: never; 257: always).  r05h:
+// always merging cost silesia-like / text blocks 10 / 30 % and saved 13 % on
+// binary records; r05i, against never: threshold 64 -5.5 % silesia-like,
+// +2.4 % text, -12 % records (96: -5.0 / +3.4 / -12; 128: -3.5 / +8.5 / -12).
 #ifndef LZ4M_CMP_TNMERGE
-#define LZ4M_CMP_TNMERGE 1
+#define LZ4M_CMP_TNMERGE 64
 #endif
 
 // length bytes after a token nibble of 15 (lz4.c:1094-1099, 1184-1194);
@@ -206,12 +221,25 @@ constexpr int kRingBytes = 16;           // A/B builds: every source read from m
 #else
 constexpr int kRingBytes = kRing + 32;   // + a mirror of the first 32 bytes
 #endif
+// LZ4M_CMP_STAGE: bytes of LDS output staging after the ring (0: none; 448
+// fits the LDS allocation the table and the ring already take, 9 waves per
+// CU).  r05h: 2-4 % slower on silesia-like / text blocks, 1 % faster on
+// binary records -- the parse's stores cost their issue, not waits (off)
+#ifndef LZ4M_CMP_STAGE
+#define LZ4M_CMP_STAGE 0
+#endif
+#ifdef LZ4M_NO_RING
+constexpr int kOB = 0;
+#else
+constexpr int kOB = LZ4M_CMP_STAGE;
+#endif
+static_assert(kOB % 16 == 0 && kOB < 16 * kWave, "staging: whole 16-byte pieces, one per lane");
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 #ifdef LZ4M_NO_RING   // A/B: no ring in LDS at all (the 16 KiB table alone, 10 waves per CU)
 #define RING_DECL lds_u8* ring = nullptr;
 #else
 #define RING_DECL                                                               \
-    __shared__ __attribute__((aligned(16))) uint8_t ring_mem[kRingBytes];       \
+    __shared__ __attribute__((aligned(16))) uint8_t ring_mem[kRingBytes + kOB];   \
     lds_u8* ring = (lds_u8*)ring_mem;
 #endif
 
@@ -433,6 +461,19 @@ __device__ __forceinline__ int32_t compress_block_w(const uint8_t* __restrict__ 
 
     int32_t staged = 0;   // LW with `stage`: bytes known to be in LDS (wave uniform)
     int32_t tnb = 0;      // 1: the next search step starts with the test of position ip (LZ4M_CMP_TNMERGE)
+    int32_t tnh = 128;    // running hit rate of the test of the next position, 1/256 units
+    // output staging (LZ4M_CMP_STAGE): output bytes [fbase, op) wait in LDS and
+    // leave in one coalesced store per lane, so that the parse's loads seldom
+    // wait for its own stores (gfx9 counts both in one in-order counter)
+    constexpr bool kStg = !LW && (LZ4M_CMP_STAGE > 0);
+    lds_u8* const ob = kStg ? ring + kRingBytes : nullptr;
+    int32_t fbase = 0;
+    auto ob_flush = [&]() __attribute__((always_inline)) {
+        const int32_t pend = op - fbase;
+        const int32_t c = 16 * (int32_t)lane;
+        if (c < pend) CST(gbl_put_c(dst + fbase + c, lds_ld16(ob + c), pend - c));
+        fbase = op;
+    };
     CP_DECL
     if (n < kMinLength) goto last_literals;                    // lz4.c:981
 
@@ -443,8 +484,6 @@ __device__ __forceinline__ int32_t compress_block_w(const uint8_t* __restrict__ 
 
     for (;;) {
         int32_t match;
-        int32_t tok_pos;
-        uint32_t tok_hi;   // literal-length nibble; the token byte is written once, with the match nibble
         uint32_t PM, GM;
         {   // ---- search (lz4.c:1016-1075), 64 attempts per wave step ----
             SI k0 = 0;
@@ -538,6 +577,7 @@ __device__ __forceinline__ int32_t compress_block_w(const uint8_t* __restrict__ 
                 const bool hit = ok && gv.x == pv.x;
                 const uint64_t hmask = __ballot(hit);
                 const int f = hmask ? __builtin_ctzll(hmask) : nvalid;   // last lane processed: f (or all valid)
+                if (LZ4M_CMP_TNMERGE > 0 && tnb && k0 == 0) tnh += ((int32_t)(hmask & 1u) * 256 - tnh) >> 3;
                 // one write per touched bucket: the group's last lane <= f
                 // inserts its position; a group entirely after f restores
                 if (valid && (((int)lane <= f && succ > f) || ((int)lane > f && pred < 0)))
@@ -585,56 +625,15 @@ __device__ __forceinline__ int32_t compress_block_w(const uint8_t* __restrict__ 
             CP_COUNT(9, 1);
         }
 
-        {   // ---- literal run (lz4.c:1083-1107) ----
+    next_match:   // (the separate test of the next position: anchor == ip, no literals)
+        {   // ---- match length, then the sequence's bytes (lz4.c:1083-1197) ----
+            // LZ4_count(ip+4, match+4, matchlimit) first (it reads the source
+            // only), so that the sequence's size is known before any byte of it
+            // is written: bytes 4..15 of P/G, then 4 bytes per lane from HBM; a
+            // match in the history runs on into the block (lz4.c:1141-1153) --
+            // the window is contiguous
             const int32_t lit = ip - anchor;
-            tok_pos = op;
-            op += 1;
-            if (limited && op + lit + (2 + 1 + 5) + lit / 255 > cap) return 0;
-            if (lit >= 15) {
-                tok_hi = 15 << 4;
-                op = put_len(dst, op, lit - 15, lane);
-            } else {
-                tok_hi = (uint32_t)lit << 4;
-            }
-            uint8_t* d = dst + op;
-            const int32_t d_room = cap - op;
-            for (int32_t b0 = 0; b0 < lit; b0 += 16 * kWave) {
-                const int32_t q = b0 + 16 * (int32_t)lane;
-                if (q < lit) {
-                    const int32_t p = anchor + q;
-                    u32x4 v;
-                    if constexpr (LW) {
-                        v = lw_ld16(w, p);
-                    } else {
-                        const bool in = W.has(p, 16);
-                        v = ring_fetch16(W, p);
-                        if (__any(!in)) {
-                            const u32x4 gv = ld16_win(w, p, iend);
-                            if (!in) v = gv;
-                        }
-                    }
-                    if (lit - q >= 16 || d_room - q >= 16) {
-                        CST(st16(d + q, v));
-                    } else {
-                        for (int32_t j = 0; j < lit - q; ++j) CST(d[q + j] = (uint8_t)byte_of(v, (int)j));
-                    }
-                }
-            }
-            op += lit;
-            CP_MARK(4);
-        }
-
-    next_match:
-        {   // ---- offset + match length (lz4.c:1125-1197) ----
             const uint32_t off = (uint32_t)(ip - match);
-            if (lane == 0) {
-                CST(dst[op] = (uint8_t)off);
-                CST(dst[op + 1] = (uint8_t)(off >> 8));
-            }
-            op += 2;
-            // LZ4_count(ip+4, match+4, matchlimit): bytes 4..15 of P/G first,
-            // then 4 bytes per lane from HBM; a match in the history runs on
-            // into the block (lz4.c:1141-1153) -- the window is contiguous
             const int32_t avail = matchlimit - (pbase + 4);
             int32_t c = eq12(P, G);
             if (c > avail) c = avail;
@@ -682,24 +681,100 @@ __device__ __forceinline__ int32_t compress_block_w(const uint8_t* __restrict__ 
                 CP_COUNT(12, 1);
             }
             mcode = (int32_t)uni((uint32_t)mcode);
-            ip += mcode + 4;
-            if (limited && op + (1 + 5) + (mcode + 240) / 255 > cap) return 0;
-            uint32_t tok_lo;
-            if (mcode >= 15) {
-                tok_lo = 15;
-                op = put_len(dst, op, mcode - 15, lane);
-            } else {
-                tok_lo = (uint32_t)mcode;
-            }
-            if (lane == 0) CST(dst[tok_pos] = (uint8_t)(tok_hi + tok_lo));
             CP_MARK(5);
+            // the output checks, in the reference's order (lz4.c:1085-1089, 1184-1190;
+            // for the test of the next position the first is implied by the second)
+            if (limited && op + 1 + lit + (2 + 1 + 5) + lit / 255 > cap) return 0;
+            const int32_t llb = lit >= 15 ? (lit - 15) / 255 + 1 : 0;   // literal-length bytes
+            const int32_t mlb = mcode >= 15 ? (mcode - 15) / 255 + 1 : 0;   // match-length bytes
+            if (limited && op + 1 + llb + lit + 2 + (1 + 5) + (mcode + 240) / 255 > cap) return 0;
+            const int32_t size = 1 + llb + lit + 2 + mlb;
+            const uint32_t tok = ((uint32_t)(lit < 15 ? lit : 15) << 4) | (uint32_t)(mcode < 15 ? mcode : 15);
+            if constexpr (kStg) {
+                if (op - fbase + size + 16 > kOB) ob_flush();   // at a sequence boundary
+            }
+            if (kStg && size + 16 <= kOB) {
+                // into the staging buffer: every write lands before [op - fbase + size + 16)
+                lds_u8* const o = ob + (op - fbase);
+                if (lane == 0) o[0] = (uint8_t)tok;
+                int32_t x = 1;
+                if (llb) {
+                    const int32_t n255 = llb - 1;
+                    for (int32_t k = lane; k < n255; k += kWave) o[1 + k] = 255;
+                    if (lane == 0) o[1 + n255] = (uint8_t)(lit - 15 - 255 * n255);
+                    x += llb;
+                }
+                {   // whole 16-byte pieces (the spill past the literal is overwritten below)
+                    const int32_t q = 16 * (int32_t)lane;
+                    if (q < lit) {
+                        const int32_t p = anchor + q;
+                        const bool in = W.has(p, 16);
+                        u32x4 v = ring_fetch16(W, p);
+                        if (__any(!in)) {
+                            const u32x4 gv = ld16_win(w, p, iend);
+                            if (!in) v = gv;
+                        }
+                        lds_st16(o + x + q, v);
+                    }
+                }
+                x += lit;
+                if (lane == 0) {
+                    o[x] = (uint8_t)off;
+                    o[x + 1] = (uint8_t)(off >> 8);
+                }
+                x += 2;
+                if (mlb) {
+                    const int32_t n255 = mlb - 1;
+                    for (int32_t k = lane; k < n255; k += kWave) o[x + k] = 255;
+                    if (lane == 0) o[x + n255] = (uint8_t)(mcode - 15 - 255 * n255);
+                }
+                op += size;
+            } else {
+                // straight to dst (a sequence larger than the staging buffer, or LW)
+                const int32_t tok_pos = op;
+                op += 1;
+                if (llb) op = put_len(dst, op, lit - 15, lane);
+                uint8_t* d = dst + op;
+                const int32_t d_room = cap - op;
+                for (int32_t b0 = 0; b0 < lit; b0 += 16 * kWave) {
+                    const int32_t q = b0 + 16 * (int32_t)lane;
+                    if (q < lit) {
+                        const int32_t p = anchor + q;
+                        u32x4 v;
+                        if constexpr (LW) {
+                            v = lw_ld16(w, p);
+                        } else {
+                            const bool in = W.has(p, 16);
+                            v = ring_fetch16(W, p);
+                            if (__any(!in)) {
+                                const u32x4 gv = ld16_win(w, p, iend);
+                                if (!in) v = gv;
+                            }
+                        }
+                        if (lit - q >= 16 || d_room - q >= 16) {
+                            CST(st16(d + q, v));
+                        } else {
+                            for (int32_t j = 0; j < lit - q; ++j) CST(d[q + j] = (uint8_t)byte_of(v, (int)j));
+                        }
+                    }
+                }
+                op += lit;
+                if (lane == 0) {
+                    CST(dst[op] = (uint8_t)off);
+                    CST(dst[op + 1] = (uint8_t)(off >> 8));
+                }
+                op += 2;
+                if (mlb) op = put_len(dst, op, mcode - 15, lane);
+                if (lane == 0) CST(dst[tok_pos] = (uint8_t)tok);
+                if constexpr (kStg) fbase = op;
+            }
+            ip += mcode + 4;
+            CP_MARK(4);
         }
         anchor = ip;
         if (ip >= mflimit1) break;                             // lz4.c:1204
-        if (LZ4M_CMP_TNMERGE && A == 64) {   // the test of ip: lane 0 of the next search step
-            tnb = 1;
-            continue;
-        }
+        tnb = LZ4M_CMP_TNMERGE > 0 && A == 64 && tnh < LZ4M_CMP_TNMERGE;
+        if (tnb) continue;   // the test of ip: lane 0 of the next search step
 
         {   // ---- fill table, test next position (lz4.c:1207-1258) ----
             uint32_t pm;
@@ -726,16 +801,15 @@ __device__ __forceinline__ int32_t compress_block_w(const uint8_t* __restrict__ 
                 const int32_t cpos = ok ? (int32_t)cand - (int32_t)ibase : ip;
                 // (a candidate inside the ring read from there instead: -0.5 %, r04aa)
                 const u32x4 gv = LW ? lw_ld16(w, cpos) : ld16_win(w, cpos, iend);
-                if (ok && gv.x == pv.x) {
+                const bool thit = ok && gv.x == pv.x;
+                if (LZ4M_CMP_TNMERGE > 0) tnh += ((int32_t)thit * 256 - tnh) >> 3;
+                if (thit) {
                     match = cpos;
                     P = pv;
                     G = gv;
                     pbase = ip;
                     gbase = cpos;
                     back = 0;
-                    tok_pos = op;
-                    tok_hi = 0;
-                    op += 1;
                     CP_MARK(6);
                     CP_COUNT(10, 1);
                     goto next_match;
@@ -747,6 +821,7 @@ __device__ __forceinline__ int32_t compress_block_w(const uint8_t* __restrict__ 
     }
 
 last_literals:
+    if constexpr (kStg) ob_flush();
     {   // lz4.c:1266-1293
         const int32_t run = iend - anchor;
         if (limited && op + run + 1 + (run + 255 - 15) / 255 > cap) return 0;

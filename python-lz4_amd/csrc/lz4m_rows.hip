@@ -723,7 +723,9 @@ static_assert(LZ4M_ROWS_ORDER == 1, "the far-source pieces (FarSrc) are reused b
 #define LZ4M_ROWS_ENDS 1    // a round whose rows all take 16 sequences: next (ip, op) = lane 15's ends (no scans)
 #endif
 #ifndef LZ4M_ROWS_XP
-#define LZ4M_ROWS_XP 0      // timing probes, WRONG output (r05a): 2 no HBM loads in passes, 4 no late loads, 8 no far prefetch
+#define LZ4M_ROWS_XP 0      // timing probes, WRONG output (r05a): 2 no HBM loads in passes, 4 no late loads, 8 no far prefetch,
+                            // (r05i) 16 one pass without scans, 32 no literal puts, 64 no flush stores, 128 no match copies, 256 no rebase copy,
+                            // (r05j) 512 no long-match loop, 1024 no match puts, 2048 no match-source LDS reads
 #endif
 #ifndef LZ4M_ROWS_COUNTED
 #define LZ4M_ROWS_COUNTED 0   // A/B: a fixed number of memory operations per round on the common path (measured -1 %)
@@ -1110,6 +1112,7 @@ __global__ __launch_bounds__(kEWG) __attribute__((amdgpu_waves_per_eu(LZ4M_ROWS_
         const bool u = (P.fl & kFlU) != 0;
         const int32_t lit = P.lit, o = P.o;
         // literals: bytes lp.. of the input (exact, branch-free); longer ones rare
+        if (!(LZ4M_ROWS_XP & 32)) {
 #if LZ4M_LDS_ALIGN
         if (u && lit > 0) lds_put_al(HB + (o - base), XSL[0], lit, MT);
 #elif LZ4M_ROWS_LITPUT == 1
@@ -1128,6 +1131,7 @@ __global__ __launch_bounds__(kEWG) __attribute__((amdgpu_waves_per_eu(LZ4M_ROWS_
                 wait_vm0();
 #endif
             }
+        }
         }
         }
         // ---- parse the next round ahead (its far sources are requested now),
@@ -1179,11 +1183,11 @@ __global__ __launch_bounds__(kEWG) __attribute__((amdgpu_waves_per_eu(LZ4M_ROWS_
 #if LZ4M_ROWS_PUTMASK >= 3
         // one match copy (exec-masked to the ready lanes: an LDS access costs per active lane)
         auto copy_match = [&]() __attribute__((always_inline)) {
-            const u32x4 l0 = lds_ld16u(HB + (s0 >= base ? s0 - base : 0));
+            const u32x4 l0 = (LZ4M_ROWS_XP & 2048) ? u32x4{(uint32_t)s0, 0u, 0u, 0u} : lds_ld16u(HB + (s0 >= base ? s0 - base : 0));
             u32x4 v0 = far ? g0 : l0;
             if (per) v0 = period_perm(l0, PS + 8 * off);
-            LDS_PUT(HB + (m - base), v0, ml);
-            if (ml > stp) {   // the rest (matches longer than one step)
+            if (!(LZ4M_ROWS_XP & 1024)) LDS_PUT(HB + (m - base), v0, ml);
+            if (ml > stp && !(LZ4M_ROWS_XP & 512)) {   // the rest (matches longer than one step)
                 for (int32_t i = stp; i < ml; i += stp) {
                     u32x4 v = v0;
                     if (!per) {
@@ -1193,7 +1197,7 @@ __global__ __launch_bounds__(kEWG) __attribute__((amdgpu_waves_per_eu(LZ4M_ROWS_
                         // with the first; later pieces are loaded now, only where
                         // some lane needs one (this wait then covers only loads
                         // older than the round's own requests, LZ4M_ROWS_ORDER)
-                        v = lds_ld16u(HB + (sp >= base ? sp - base : 0));
+                        v = (LZ4M_ROWS_XP & 2048) ? u32x4{(uint32_t)sp, 0u, 0u, 0u} : lds_ld16u(HB + (sp >= base ? sp - base : 0));
                         if (!(LZ4M_ROWS_XP & 2)) {
                             const bool pc1 = (i == 16) & far & !late;
                             if (sp < base && pc1) v = g1;
@@ -1204,7 +1208,7 @@ __global__ __launch_bounds__(kEWG) __attribute__((amdgpu_waves_per_eu(LZ4M_ROWS_
                             }
                         }
                     }
-                    LDS_PUT(HB + (m - base + i), v, ml - i);
+                    if (!(LZ4M_ROWS_XP & 1024)) LDS_PUT(HB + (m - base + i), v, ml - i);
                 }
             }
         };
@@ -1225,9 +1229,9 @@ __global__ __launch_bounds__(kEWG) __attribute__((amdgpu_waves_per_eu(LZ4M_ROWS_
             // the start of the first pending match below (0: none)
             int32_t x1, y1;
             row_excl_max2(pend ? mend + 1 : 0, pend ? 0x3FFFFFFF - m : 0, x1, y1);
-            const bool ready = pend & ((x1 <= s0 + 1) | (y1 <= 0x3FFFFFFF - se));
+            const bool ready = (LZ4M_ROWS_XP & 16) ? pend : pend & ((x1 <= s0 + 1) | (y1 <= 0x3FFFFFFF - se));
 #if LZ4M_ROWS_PUTMASK >= 3
-            if (ready) copy_match();
+            if (ready && !(LZ4M_ROWS_XP & 128)) copy_match();
             pend = pend && !ready;
         }
 #else
@@ -1281,7 +1285,8 @@ __global__ __launch_bounds__(kEWG) __attribute__((amdgpu_waves_per_eu(LZ4M_ROWS_
             }
         }
 #else
-        for (int32_t c = F + 16 * jj; c + 16 <= opn; c += 256) st16(d + c, lds_ld16(HB + (c - base)));
+        if (!(LZ4M_ROWS_XP & 64))
+            for (int32_t c = F + 16 * jj; c + 16 <= opn; c += 256) st16(d + c, lds_ld16(HB + (c - base)));
 #endif
         F += (opn - F) & ~15;
         op = opn;
@@ -1291,7 +1296,7 @@ __global__ __launch_bounds__(kEWG) __attribute__((amdgpu_waves_per_eu(LZ4M_ROWS_
         if (nbse != base) {
             // the kept bytes lie >= kRowsH - kRowsRoom - kRowsKeep past the
             // buffer start: all reads of a group before its writes
-            for (int32_t c0 = 0; c0 < op - nbse; c0 += 1024) {
+            for (int32_t c0 = 0; c0 < ((LZ4M_ROWS_XP & 256) ? 0 : op - nbse); c0 += 1024) {
                 u32x4 v[4];
 #pragma unroll
                 for (int g = 0; g < 4; ++g) v[g] = lds_ld16(HB + (nbse - base) + c0 + 256 * g + 16 * jj);
