@@ -128,7 +128,26 @@ __device__ __forceinline__ u32x4 period_pattern(u32x4 w, uint32_t off) {
 typedef __attribute__((address_space(3))) volatile uint64_t lds_vu64;
 typedef __attribute__((address_space(3))) const uint32_t lds_cu32;
 __device__ __forceinline__ uint32_t lds_addr(const lds_u8* p) { return (uint32_t)(uintptr_t)p; }
+// LZ4M_LDS_PERM: the shifts of an aligned read / put as v_perm with one
+// selector per lane instead of a select and an alignbyte per dword, and the
+// put's data zeroed outside its bytes by the selector (0x0C) instead of an
+// AND with the mask: 2 VALU per put dword instead of 3; the read is five
+// aligned dwords (two ds_read2_b32 and one ds_read_b32) and four alignbytes
+// instead of three aligned qwords, five selects and four alignbytes
+#ifndef LZ4M_LDS_PERM
+#define LZ4M_LDS_PERM 1
+#endif
+typedef __attribute__((address_space(3))) const uint32_t lds_cu32a __attribute__((aligned(4)));
 __device__ __forceinline__ u32x4 lds_ld16a(const lds_u8* p) {
+#if LZ4M_LDS_PERM
+    {
+        const uint32_t a = lds_addr(p), r = a & 3u;
+        const lds_cu32a* q = (const lds_cu32a*)(p - r);
+        const uint32_t c0 = q[0], c1 = q[1], c2 = q[2], c3 = q[3], c4 = q[4];
+        return u32x4{__builtin_amdgcn_alignbyte(c1, c0, r), __builtin_amdgcn_alignbyte(c2, c1, r),
+                     __builtin_amdgcn_alignbyte(c3, c2, r), __builtin_amdgcn_alignbyte(c4, c3, r)};
+    }
+#endif
     const uint32_t a = lds_addr(p);
     const lds_vu64* q = (const lds_vu64*)(p - (a & 7u));
     const uint64_t x0 = q[0], x1 = q[1], x2 = q[2];
@@ -160,6 +179,31 @@ __device__ __forceinline__ void lds_put_table_init(uint32_t* tab, uint32_t lane,
 __device__ __forceinline__ void lds_put_al(lds_u8* p, u32x4 v, int32_t k, lds_cu32* tab) {
     const uint32_t a = lds_addr(p), r = a & 3u;
     const uint32_t kk = k >= 16 ? 16u : (uint32_t)k;
+#if LZ4M_LDS_PERM && LZ4M_LDS_ALIGN == 1
+    {
+        // destination dword i, byte b holds put byte 4i + b - r: v_perm of
+        // (v[i], v[i-1]) with selector byte 4 + b - r, 0x0C (zero) where the
+        // mask says the byte is not the put's
+        u32x4 m;
+        __builtin_memcpy(&m, (const uint8_t*)(tab + 4u * (r * 17u + kk)), 16);   // 16-byte aligned
+        const int32_t t4 = (int32_t)(r + kk) - 16;   // bytes in dword 4 (0..3)
+        const uint32_t m4 = t4 > 0 ? (1u << (8 * t4)) - 1u : 0u;
+        const uint32_t sb = 0x07060504u - r * 0x01010101u;
+        const uint32_t b4 = a & ~3u;
+        auto sel = [&](uint32_t mk) __attribute__((always_inline)) { return (mk & sb) | (~mk & 0x0C0C0C0Cu); };
+        const uint32_t d0 = __builtin_amdgcn_perm(v.x, v.x, sel(m.x));
+        const uint32_t d1 = __builtin_amdgcn_perm(v.y, v.x, sel(m.y));
+        const uint32_t d2 = __builtin_amdgcn_perm(v.z, v.y, sel(m.z));
+        const uint32_t d3 = __builtin_amdgcn_perm(v.w, v.z, sel(m.w));
+        const uint32_t d4 = __builtin_amdgcn_perm(0u, v.w, sel(m4));
+        asm volatile("ds_mskor_b32 %0, %1, %2 offset:0" ::"v"(b4), "v"(m.x), "v"(d0) : "memory");
+        asm volatile("ds_mskor_b32 %0, %1, %2 offset:4" ::"v"(b4), "v"(m.y), "v"(d1) : "memory");
+        asm volatile("ds_mskor_b32 %0, %1, %2 offset:8" ::"v"(b4), "v"(m.z), "v"(d2) : "memory");
+        asm volatile("ds_mskor_b32 %0, %1, %2 offset:12" ::"v"(b4), "v"(m.w), "v"(d3) : "memory");
+        asm volatile("ds_mskor_b32 %0, %1, %2 offset:16" ::"v"(b4), "v"(m4), "v"(d4) : "memory");
+        return;
+    }
+#endif
     const uint32_t s = (4u - r) & 3u;
     const bool z = r == 0;
     const uint32_t d0 = __builtin_amdgcn_alignbyte(v.x, z ? v.x : 0u, s);
