@@ -102,6 +102,16 @@ struct Table<LZ4M_TABLE_U16_HASH4> {   // 8192 x u16 (lz4.c:756-762, 839-843)
         ((volatile lds_t16*)t)[h] = (uint16_t)v;
     }
     static constexpr bool kDistCheck = false;   // lz4.c:1064, LZ4_DISTANCE_MAX == 65535
+    // store v, return the entry before it: a masked OR with return on the
+    // enclosing dword (no 16-bit exchange exists)
+    __device__ static __forceinline__ uint32_t xchg(uint16_t* t, uint32_t h, uint32_t v) {
+        const uint32_t a = (uint32_t)(uintptr_t)((lds_t16*)t + h) & ~3u, sh = (h & 1u) * 16u;
+        uint32_t old;
+        // (the wait inside: the compiler does not count an asm's LDS return)
+        asm volatile("ds_mskor_rtn_b32 %0, %1, %2, %3\n\ts_waitcnt lgkmcnt(0)"
+                     : "=v"(old) : "v"(a), "v"(0xFFFFu << sh), "v"((v & 0xFFFFu) << sh) : "memory");
+        return (old >> sh) & 0xFFFFu;
+    }
 };
 
 template <>
@@ -119,7 +129,24 @@ struct Table<LZ4M_TABLE_U32_HASH5> {   // 4096 x u32 (lz4.c:764-774, 834-838)
     __device__ static __forceinline__ uint32_t get_v(uint16_t* t, uint32_t h) { return ((volatile lds_t32*)t)[h]; }
     __device__ static __forceinline__ void put_v(uint16_t* t, uint32_t h, uint32_t v) { ((volatile lds_t32*)t)[h] = v; }
     static constexpr bool kDistCheck = true;
+    __device__ static __forceinline__ uint32_t xchg(uint16_t* t, uint32_t h, uint32_t v) {
+        return __hip_atomic_exchange((lds_t32*)t + h, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
 };
+
+// LZ4M_CMP_XCHG: the search step inserts its 64 positions with one LDS
+// exchange per lane; lanes of a wave that hit the same bucket are applied in
+// lane order (gfx950: every one of 33.5 M instructions of random collision
+// patterns, tools/micro/lds_xchg_order.hip, r05l), so each lane reads back
+// exactly the entry the serial loop (lz4.c:1016-1075) would read: the table's
+// for the first lane of a bucket, the previous lane's position for the others.
+// After the step's first hit f, the first lane after f in each bucket writes
+// back what it read (positions increase with the lane, so that lane is the one
+// whose read value is below lane f+1's position).  Replaces a read, a probe
+// write, a read back and a loop over the colliding groups.
+#ifndef LZ4M_CMP_XCHG
+#define LZ4M_CMP_XCHG 1
+#endif
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 __device__ __forceinline__ int64_t uni64(int64_t v) {
@@ -527,7 +554,12 @@ __device__ __forceinline__ int32_t compress_block_w(const uint8_t* __restrict__ 
                                             __builtin_amdgcn_alignbyte(pv.y, pv.x, 2), 0u, 0u};
                     T::put_v(tab, T::hash_v(pv2), cur - 2u);
                 }
-                if (valid) {
+                if (LZ4M_CMP_XCHG) {
+                    if (valid) {
+                        h = T::hash_v(pv);
+                        old = T::xchg(tab, h, cur);
+                    }
+                } else if (valid) {
                     h = T::hash_v(pv);
                     old = T::get_v(tab, h);
                     T::put_v(tab, h, lane);
@@ -536,7 +568,7 @@ __device__ __forceinline__ int32_t compress_block_w(const uint8_t* __restrict__ 
                 CP_MARK(0);
                 // per hash group: nearest earlier (pred) and later (succ) lane
                 int pred = -1, succ = 1 << 20;
-                uint64_t todo = __ballot(rb != lane);
+                uint64_t todo = LZ4M_CMP_XCHG ? 0ull : __ballot(rb != lane);
                 while (todo) {
                     CP_COUNT(11, 1);
                     const int l = __builtin_ctzll(todo);
@@ -578,10 +610,17 @@ __device__ __forceinline__ int32_t compress_block_w(const uint8_t* __restrict__ 
                 const uint64_t hmask = __ballot(hit);
                 const int f = hmask ? __builtin_ctzll(hmask) : nvalid;   // last lane processed: f (or all valid)
                 if (LZ4M_CMP_TNMERGE > 0 && tnb && k0 == 0) tnh += ((int32_t)(hmask & 1u) * 256 - tnh) >> 3;
-                // one write per touched bucket: the group's last lane <= f
-                // inserts its position; a group entirely after f restores
-                if (valid && (((int)lane <= f && succ > f) || ((int)lane > f && pred < 0)))
+                if (LZ4M_CMP_XCHG) {
+                    // undo the lanes after f: the first of each bucket restores
+                    if (f < nvalid) {
+                        const uint32_t cf1 = (uint32_t)__builtin_amdgcn_readlane((int)cur, f < 63 ? f + 1 : 63);
+                        if (valid && (int)lane > f && old < cf1) T::put_v(tab, h, old);
+                    }
+                } else if (valid && (((int)lane <= f && succ > f) || ((int)lane > f && pred < 0))) {
+                    // one write per touched bucket: the group's last lane <= f
+                    // inserts its position; a group entirely after f restores
                     T::put_v(tab, h, (int)lane <= f ? cur : old);
+                }
                 if (pf) fill_commit(W, fv, lane);
                 CP_MARK(2);
                 if (hmask) {

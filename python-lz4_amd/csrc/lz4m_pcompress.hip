@@ -252,12 +252,40 @@ struct Chunk {
     uint32_t bp, bc;  // 4 bytes before p / before cand
 };
 
+// LZ4M_PC_XCHG: each lane exchanges its position into its bucket and reads
+// back the entry before it; one instruction's lanes on one LDS address are
+// applied in lane order on gfx950 (tools/micro/lds_xchg_order.hip, r05l), so
+// that is the most recent earlier position with the same hash -- the
+// candidate -- and the table ends holding each bucket's last position, as
+// with the per-hash-bit ballots it replaces.
+#ifndef LZ4M_PC_XCHG
+#define LZ4M_PC_XCHG 1
+#endif
+
 template <bool BIG, int HB>
 __device__ __forceinline__ void chunk_issue(Chunk& C, const uint8_t* s, uint32_t* table32, int32_t p0, uint32_t v,
                                             int32_t N, int32_t mlast, uint32_t lane) {
     const int32_t p = p0 + (int32_t)lane;
     const bool act = p + 4 <= N;
     const uint32_t h = act ? phash<HB>(v) : (1u << HB);
+#if LZ4M_PC_XCHG
+    int32_t cand = -1;
+    if (act) {
+        uint32_t old;
+        if (BIG) {
+            typedef __attribute__((address_space(3))) uint32_t l32;
+            old = __hip_atomic_exchange((l32*)table32 + h, (uint32_t)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            cand = old == 0xFFFFFFFFu ? -1 : (int32_t)old;
+        } else {
+            typedef __attribute__((address_space(3))) uint16_t l16;
+            const uint32_t a = (uint32_t)(uintptr_t)((l16*)table32 + h) & ~3u, sh = (h & 1u) * 16u;
+            asm volatile("ds_mskor_rtn_b32 %0, %1, %2, %3\n\ts_waitcnt lgkmcnt(0)"
+                         : "=v"(old) : "v"(a), "v"(0xFFFFu << sh), "v"(((uint32_t)p & 0xFFFFu) << sh) : "memory");
+            old = (old >> sh) & 0xFFFFu;
+            cand = old == kEmpty ? -1 : (int32_t)old;
+        }
+    }
+#else
     // lanes with the same hash (one ballot per hash bit), hence the nearest
     // earlier one (the candidate) and whether a later one exists (then this
     // lane does not write the table)
@@ -276,6 +304,7 @@ __device__ __forceinline__ void chunk_issue(Chunk& C, const uint8_t* s, uint32_t
             table16[h] = (uint16_t)p;
         }
     }
+#endif
     C.v = v;
     C.cand = cand;
     // LZ4_DISTANCE_MAX (lz4.c:1064): only checkable past 64 KiB
