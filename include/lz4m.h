@@ -35,6 +35,10 @@ extern "C" {
 typedef struct ihipStream_t* lz4m_stream_t;   /* == hipStream_t */
 
 #define LZ4M_EINVAL 0x10000
+/* The device failed the LDS lane-order self-test (lz4m_selftest_lds_order):
+ * the compressors' search steps rely on one instruction's same-address LDS
+ * atomics being applied in lane order (gfx950 does), and refuse to run. */
+#define LZ4M_EDEVICE 0x10001
 
 /* Match-finder table layouts:
  *   U16_HASH4: LZ4_compress_default on blocks < 65547 B (lz4.c:1353-1354),
@@ -59,6 +63,13 @@ typedef struct ihipStream_t* lz4m_stream_t;   /* == hipStream_t */
 
 /* LZ4_compressBound (lz4.h:212 / lz4.c:730). */
 int lz4m_compress_bound(int input_size);
+
+/* Runs the LDS lane-order self-test on the current device (synchronous, its
+ * own stream): returns the number of test instructions whose same-address
+ * exchanges were not applied in lane order (0 = the compressors' insert
+ * order holds), or a negative HIP error.  Every compression entry point runs
+ * it once per process and returns LZ4M_EDEVICE if it fails. */
+int lz4m_selftest_lds_order(void);
 
 /*
  * Batched lz4.block.compress(source, dict=D) for the non-HC modes

@@ -188,7 +188,8 @@ __device__ __forceinline__ void lds_put_al(lds_u8* p, u32x4 v, int32_t k, lds_cu
         __builtin_memcpy(&m, (const uint8_t*)(tab + 4u * (r * 17u + kk)), 16);   // 16-byte aligned
         const int32_t t4 = (int32_t)(r + kk) - 16;   // bytes in dword 4 (0..3)
         const uint32_t m4 = t4 > 0 ? (1u << (8 * t4)) - 1u : 0u;
-        const uint32_t sb = 0x07060504u - r * 0x01010101u;
+        // r replicated into every byte by one v_perm (a v_mul_lo_u32 is quarter rate)
+        const uint32_t sb = 0x07060504u - __builtin_amdgcn_perm(0u, r, 0u);
         const uint32_t b4 = a & ~3u;
         auto sel = [&](uint32_t mk) __attribute__((always_inline)) { return (mk & sb) | (~mk & 0x0C0C0C0Cu); };
         const uint32_t d0 = __builtin_amdgcn_perm(v.x, v.x, sel(m.x));
@@ -199,8 +200,10 @@ __device__ __forceinline__ void lds_put_al(lds_u8* p, u32x4 v, int32_t k, lds_cu
         asm volatile("ds_mskor_b32 %0, %1, %2 offset:0" ::"v"(b4), "v"(m.x), "v"(d0) : "memory");
         asm volatile("ds_mskor_b32 %0, %1, %2 offset:4" ::"v"(b4), "v"(m.y), "v"(d1) : "memory");
         asm volatile("ds_mskor_b32 %0, %1, %2 offset:8" ::"v"(b4), "v"(m.z), "v"(d2) : "memory");
-        asm volatile("ds_mskor_b32 %0, %1, %2 offset:12" ::"v"(b4), "v"(m.w), "v"(d3) : "memory");
-        asm volatile("ds_mskor_b32 %0, %1, %2 offset:16" ::"v"(b4), "v"(m4), "v"(d4) : "memory");
+        if (!LZ4M_LDS_SKIP || __any(m.w != 0u))
+            asm volatile("ds_mskor_b32 %0, %1, %2 offset:12" ::"v"(b4), "v"(m.w), "v"(d3) : "memory");
+        if (!LZ4M_LDS_SKIP || __any(m4 != 0u))
+            asm volatile("ds_mskor_b32 %0, %1, %2 offset:16" ::"v"(b4), "v"(m4), "v"(d4) : "memory");
         return;
     }
 #endif

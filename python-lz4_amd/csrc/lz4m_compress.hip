@@ -25,6 +25,7 @@
 #include "lz4m_worker.h"
 
 #include <chrono>
+#include <mutex>
 #include <type_traits>
 
 #include <stdio.h>
@@ -1409,12 +1410,83 @@ __global__ __launch_bounds__(256) void compress_worker(Mailbox* mb, uint8_t* hd,
     }
 }
 
+// ---- the lane-order self-test (LZ4M_CMP_XCHG, LZ4M_PC_XCHG rest on it) ----
+// Every wave runs 64 instructions of each exchange form the compressors use
+// (ds_wrxchg_rtn_b32 on 32-bit entries, ds_mskor_rtn_b32 on 16-bit halves)
+// with pseudo-random bucket collisions, and counts the instructions whose
+// lanes did not each read back the nearest lower lane of their bucket.
+__global__ __launch_bounds__(256) void lds_order_kernel(uint32_t seed, uint32_t* bad) {
+    __shared__ uint32_t tab[4][64];
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    uint32_t nbad = 0;
+    for (int it = 0; it < 128; ++it) {
+        tab[w][lane] = 0;
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        uint32_t x = (seed + 7919u * (uint32_t)it + 104729u * (blockIdx.x * 4u + w)) * 2654435761u ^ (lane * 40503u);
+        x ^= x >> 13;
+        x *= 0x5bd1e995u;
+        x ^= x >> 15;
+        const uint32_t nb = 1u << (it & 6);   // 1 .. 64 buckets
+        const uint32_t h = x & (nb - 1u);
+        uint32_t prev;
+        if (it & 1) {
+            const uint32_t a = (uint32_t)(uintptr_t)((lds_t16*)&tab[w][0] + h) & ~3u, sh = (h & 1u) * 16u;
+            uint32_t old;
+            asm volatile("ds_mskor_rtn_b32 %0, %1, %2, %3\n\ts_waitcnt lgkmcnt(0)"
+                         : "=v"(old) : "v"(a), "v"(0xFFFFu << sh), "v"((lane + 1u) << sh) : "memory");
+            prev = (old >> sh) & 0xFFFFu;
+        } else {
+            prev = __hip_atomic_exchange((lds_t32*)&tab[w][h], lane + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        uint32_t exp = 0;
+        for (int l = 0; l < 64; ++l) {
+            const uint32_t hl = (uint32_t)__shfl((int)h, l);
+            if (l < (int)lane && hl == h) exp = (uint32_t)l + 1u;
+        }
+        if (__ballot(prev != exp)) ++nbad;
+    }
+    if (lane == 0 && nbad) atomicAdd(bad, nbad);
+}
+
 }  // namespace lz4m
 
 using namespace lz4m;
 
+extern "C" int lz4m_selftest_lds_order(void) {
+    uint32_t* d = nullptr;
+    hipStream_t s = nullptr;
+    uint32_t h = 0;
+    int rc = (int)hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+    if (rc == 0) rc = (int)hipMalloc(&d, sizeof(uint32_t));
+    if (rc == 0) rc = (int)hipMemsetAsync(d, 0, sizeof(uint32_t), s);
+    if (rc == 0) {
+        hipLaunchKernelGGL(lds_order_kernel, dim3(256), dim3(256), 0, s, 0x9E3779B9u, d);
+        rc = (int)hipGetLastError();
+    }
+    if (rc == 0) rc = (int)hipMemcpyAsync(&h, d, sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+    if (rc == 0) rc = (int)hipStreamSynchronize(s);
+    if (d) (void)hipFree(d);
+    if (s) (void)hipStreamDestroy(s);
+    return rc ? -rc : (int)h;
+}
+
+// 0 once the current process's device passed the lane-order self-test, else
+// LZ4M_EDEVICE (the exact compressor would not reproduce the reference's
+// bytes); run once per process, at the first compression
+static int lds_order_check() {
+    static std::once_flag once;
+    static int verdict = 0;
+    std::call_once(once, [] {
+        const int r = lz4m_selftest_lds_order();
+        verdict = r == 0 ? 0 : LZ4M_EDEVICE;
+        if (r != 0) fprintf(stderr, "lz4m: LDS lane-order self-test failed (%d): compression disabled\n", r);
+    });
+    return verdict;
+}
+
 extern "C" int lz4m_compress_worker_launch(Mailbox* mb, uint8_t* hd, uint8_t* dbuf, uint64_t idle_ticks,
                                            uint64_t life_ticks, hipStream_t stream) {
+    if (const int e = lds_order_check()) return e;
     hipLaunchKernelGGL(compress_worker, dim3(1), dim3(256), 0, stream, mb, hd, dbuf, idle_ticks, life_ticks);
     return (int)hipGetLastError();
 }
@@ -1428,6 +1500,7 @@ extern "C" int lz4m_compress_solo(const uint8_t* d_src, int32_t len, uint8_t* d_
                                   int32_t* d_out_len, int table, int acceleration, uint8_t* h_out,
                                   int32_t* h_done, lz4m_stream_t stream) {
     if (len < 0 || len > kSoloMax || cap < 0) return LZ4M_EINVAL;
+    if (const int e = lds_order_check()) return e;
     if (acceleration < 1) acceleration = 1;        // lz4.c:1350-1351
     if (acceleration > 65537) acceleration = 65537;
     hipStream_t s = (hipStream_t)stream;
@@ -1460,6 +1533,7 @@ extern "C" int lz4m_compress_batch(const uint8_t* d_src, const int64_t* d_src_of
                                    lz4m_stream_t stream) {
     if (n < 0) return LZ4M_EINVAL;
     if (n == 0) return 0;
+    if (const int e = lds_order_check()) return e;
     if (acceleration < 1) acceleration = 1;        // lz4.c:1350-1351
     if (acceleration > 65537) acceleration = 65537;
     const uint32_t grid = (uint32_t)(n < (1ll << 30) ? n : (1ll << 30));
@@ -1505,6 +1579,7 @@ static int compress_dict_launch(const uint8_t* d_src, const int64_t* d_src_off, 
                                 int prefix, lz4m_stream_t stream) {
     if (n < 0) return LZ4M_EINVAL;
     if (n == 0) return 0;
+    if (const int e = lds_order_check()) return e;
     if (acceleration < 1) acceleration = 1;
     if (acceleration > 65537) acceleration = 65537;
     const uint32_t grid = (uint32_t)(n < (1ll << 30) ? n : (1ll << 30));
@@ -1568,6 +1643,9 @@ extern "C" int lz4m_compress_linked_batch(const uint8_t* d_src, const int64_t* d
                                           int mode, void* d_work, size_t work_bytes, lz4m_stream_t stream) {
     if (n < 0 || (mode != LZ4M_LINKED_SERIAL && mode != LZ4M_LINKED_SPECULATIVE)) return LZ4M_EINVAL;
     if (n == 0) return 0;
+    if (mode == LZ4M_LINKED_SPECULATIVE && (d_work == nullptr || work_bytes < lz4m_compress_linked_workspace_size(n)))
+        return LZ4M_EINVAL;
+    if (const int e = lds_order_check()) return e;
     if (acceleration < 1) acceleration = 1;
     if (acceleration > 65537) acceleration = 65537;
     hipStream_t s = (hipStream_t)stream;

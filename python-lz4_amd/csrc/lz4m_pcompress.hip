@@ -257,9 +257,10 @@ struct Chunk {
 // applied in lane order on gfx950 (tools/micro/lds_xchg_order.hip, r05l), so
 // that is the most recent earlier position with the same hash -- the
 // candidate -- and the table ends holding each bucket's last position, as
-// with the per-hash-bit ballots it replaces.
+// with the per-hash-bit ballots it replaces.  r05n: 0.8 % slower than the
+// ballots (the 16-bit form's return needs an explicit LDS wait), so off.
 #ifndef LZ4M_PC_XCHG
-#define LZ4M_PC_XCHG 1
+#define LZ4M_PC_XCHG 0
 #endif
 
 template <bool BIG, int HB>

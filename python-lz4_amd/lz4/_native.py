@@ -42,6 +42,7 @@ def _declare(lib) -> None:
     vp, i32, i64, u32 = C.c_void_p, C.c_int, C.c_int64, C.c_uint32
     sig = {
         "lz4m_compress_bound": ([i32], i32),
+        "lz4m_selftest_lds_order": ([], i32),
         "lz4m_version_number": ([], i32),
         "lz4m_version_string": ([], C.c_char_p),
         "lz4m_decompress_batch": ([vp, vp, vp, vp, vp, vp, vp, i64, vp], i32),

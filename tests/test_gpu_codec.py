@@ -214,6 +214,15 @@ def test_xxh32_batch(gpu, oracle, corpus):
         assert got == [oracle.xxh32(b, seed) for b in items]
 
 
+def test_lds_lane_order_selftest(gpu):
+    """The exact and parallel-parse compressors insert a search step's
+    positions with one LDS exchange per lane and rely on the lanes of one
+    instruction that hit the same entry being applied in lane order (the
+    serial insert order of lz4.c:1016-1075).  The library runs this check
+    once per process before compressing; here it must report no violation."""
+    assert N.lib().lz4m_selftest_lds_order() == 0
+
+
 def test_xxh32_batch_page(gpu, oracle):
     """The quad-per-item batch kernel on a config-5-like page: 4 101 items
     (not a multiple of the 16 items a wave takes) of 0..70 000 bytes at any
