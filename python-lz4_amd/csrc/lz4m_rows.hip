@@ -719,6 +719,13 @@ constexpr int32_t kRowsH = LZ4M_ROWS_H;
 #define LZ4M_ROWS_ORDER 1   // 1 (required: FarSrc is shared by P and Q): parse ahead after this round's passes
 #endif
 static_assert(LZ4M_ROWS_ORDER == 1, "the far-source pieces (FarSrc) are reused by the round parsed ahead");
+#ifndef LZ4M_ROWS_OFFLDS
+// 1: the match offset read back from the literal's LDS slot (72 VALU fewer
+// in the kernel).  r05q: the first rows test ended in an illegal memory
+// access with it on; cause not found (the ISA's offsets match the select
+// form's), so it stays off and is not run again until it is
+#define LZ4M_ROWS_OFFLDS 0
+#endif
 #ifndef LZ4M_ROWS_ENDS
 #define LZ4M_ROWS_ENDS 1    // a round whose rows all take 16 sequences: next (ip, op) = lane 15's ends (no scans)
 #endif
@@ -817,9 +824,25 @@ __device__ __forceinline__ void parse_round(PSeq& P, int32_t jj, int32_t r, int3
     const int32_t po = lp + lit;
     const int32_t mlc = (int32_t)(tok & 15u);
     // offset and first match-length byte: from wa for lit <= 12, else from wa|wb
+#if LZ4M_ROWS_OFFLDS
+    // (the literal's 32 bytes go to the lane's LDS slot first; the offset is
+    // its byte lit: two aligned dwords read back and one alignbyte, instead of
+    // selecting among the 8 dwords of wa|wb)
+    const uint32_t sh = (uint32_t)lp;
+    XS[0] = u32x4{__builtin_amdgcn_alignbyte(wa.y, wa.x, sh), __builtin_amdgcn_alignbyte(wa.z, wa.y, sh),
+                 __builtin_amdgcn_alignbyte(wa.w, wa.z, sh), __builtin_amdgcn_alignbyte(wb.x, wa.w, sh)};
+    XS[1] = u32x4{__builtin_amdgcn_alignbyte(wb.y, wb.x, sh), __builtin_amdgcn_alignbyte(wb.z, wb.y, sh),
+                 __builtin_amdgcn_alignbyte(wb.w, wb.z, sh), __builtin_amdgcn_alignbyte(0u, wb.w, sh)};
+    const uint32_t lq = (uint32_t)(lit < 28 ? lit : 28);
+    const lds_cu32a* xd = (const lds_cu32a*)XS;
+    const uint32_t q0 = lq >> 2, q1 = q0 < 7u ? q0 + 1u : 7u;   // (lq = 28: one dword, shift 0)
+    const uint32_t dwo = __builtin_amdgcn_alignbyte(xd[q1], xd[q0], lq & 3u);
+    const uint32_t bsh = 8u * ((uint32_t)lit - lq);
+#else
     const uint32_t pq = (uint32_t)(po < 28 ? po : 28);
     const uint32_t dwo = lit <= 12 ? window_dword(wa, (uint32_t)po) : dword32(wa, wb, pq);
     const uint32_t bsh = 8u * ((uint32_t)po - pq);
+#endif
     int32_t off = (int32_t)((dwo >> bsh) & 0xFFFFu);
     const int32_t e0 = (int32_t)((dwo >> (bsh + 16)) & 0xFFu);
     int32_t ml = mlc + (mlc == 15 ? e0 : 0);
@@ -869,11 +892,13 @@ __device__ __forceinline__ void parse_round(PSeq& P, int32_t jj, int32_t r, int3
         // the second piece [s0 + 16, s0 + 32) is flushed too (not late: s0 + 32 <= F)
         FS.g1 = ld16(d + (pf & (ml > 16) ? s0 + 16 : 0));
     }
+#if !LZ4M_ROWS_OFFLDS
     const uint32_t sh = (uint32_t)lp;
     XS[0] = u32x4{__builtin_amdgcn_alignbyte(wa.y, wa.x, sh), __builtin_amdgcn_alignbyte(wa.z, wa.y, sh),
                  __builtin_amdgcn_alignbyte(wa.w, wa.z, sh), __builtin_amdgcn_alignbyte(wb.x, wa.w, sh)};
     XS[1] = u32x4{__builtin_amdgcn_alignbyte(wb.y, wb.x, sh), __builtin_amdgcn_alignbyte(wb.z, wb.y, sh),
                  __builtin_amdgcn_alignbyte(wb.w, wb.z, sh), __builtin_amdgcn_alignbyte(0u, wb.w, sh)};
+#endif
     P.t = t + lp;
     P.lit = lit;
     P.off = off;

@@ -394,6 +394,51 @@ def xxh32_of_device(t: torch.Tensor, n: int, seed: int = 0, wait_stream=None, ch
     return st.digest()
 
 
+def xxh32_of_device_spans(t: torch.Tensor, spans, seed: int = 0, state: "HostXXH32 | None" = None,
+                          chunk: int = 64 << 20) -> "HostXXH32":
+    """Continue an XXH32 on a host core over device bytes t[lo:hi] of each
+    span (lo, hi, event) in order, the spans contiguous: a span's copies are
+    queued behind its event (the device work that writes those bytes), so
+    the hash follows the producer instead of waiting for all of it.  Returns
+    the state (``.digest()`` ends it).  The copy and pinned-buffer scheme is
+    xxh32_of_device's."""
+    st = state if state is not None else HostXXH32(seed)
+    pieces = []
+    for lo, hi, ev in spans:
+        for a in range(lo, hi, chunk):
+            pieces.append((a, min(hi, a + chunk), ev))
+    if not pieces:
+        return st
+    dev = t.device
+    side = torch.cuda.Stream(dev, priority=int(os.environ.get("LZ4M_HASH_STREAM_PRIORITY", "-1")))
+    bufs = _pinned_pair(chunk)
+    evs = [torch.cuda.Event(), torch.cuda.Event()]
+    flat = t.view(-1)
+    waited = set()
+
+    def issue(i):
+        lo, hi, ev = pieces[i]
+        with torch.cuda.stream(side):
+            if ev is not None and id(ev) not in waited:
+                side.wait_event(ev)
+                waited.add(id(ev))
+            bufs[i & 1][: hi - lo].copy_(flat[lo:hi], non_blocking=True)
+            evs[i & 1].record(side)
+
+    try:
+        issue(0)
+        for i, (lo, hi, _ev) in enumerate(pieces):
+            if i + 1 < len(pieces):
+                issue(i + 1)
+            evs[i & 1].synchronize()
+            st.update_ptr(bufs[i & 1].data_ptr(), hi - lo)
+    finally:
+        for e in evs:
+            e.synchronize()
+        _pinned_release(chunk, bufs)
+    return st
+
+
 # ------------------------------------------------------------ host <-> device
 # Large host <-> device moves (the drop-in frame calls on Python bytes) go
 # through two pinned chunks: lz4m_host_copy fills / drains a chunk with a few

@@ -383,9 +383,9 @@ def decompress(data, return_bytearray=False, return_bytes_read=False):
     if nb:
         d_frame = N.to_device(mv, dev, pad=16)
         t = lambda v, dt: torch.tensor(v, dtype=dt, device=dev)   # noqa: E731
-        out_t, total, first_err = _decode_records(
-            d_frame, info, nb, t([r[1] for r in recs], torch.int64), t([r[2] for r in recs], torch.int32),
-            t([r[0] for r in recs], torch.bool), t([r[3] for r in recs], torch.int64))
+        args = (d_frame, info, nb, t([r[1] for r in recs], torch.int64), t([r[2] for r in recs], torch.int32),
+                t([r[0] for r in recs], torch.bool), t([r[3] for r in recs], torch.int64))
+        out_t, total, first_err = _decode_records(*args)
     _frame_errors(first_err, state, info, total)
     bytes_read = state[1]
     host_hash = info["content_checksum"] and not (total and _content_on_gpu())
@@ -442,16 +442,21 @@ def decompress_device(d_frame: torch.Tensor, n: int | None = None, stream=None) 
         out = decompress(d_frame[:n].cpu().numpy().tobytes())
         return torch.frombuffer(bytearray(out), dtype=torch.uint8).to(dev) if out else \
             torch.empty(0, dtype=torch.uint8, device=dev)
-    out_t, total, first_err = None, 0, None
+    out_t, total, first_err, got = None, 0, None, None
     if nb:
         crc_pos = rec_pos[:nb] + rec_len[:nb].to(torch.int64) if crc else torch.full((nb,), -1, dtype=torch.int64,
                                                                                       device=dev)
-        out_t, total, first_err = _decode_records(d_frame, info, nb, rec_pos[:nb], rec_len[:nb],
-                                                  rec_raw[:nb].to(torch.bool), crc_pos)
+        follow = bool(info["content_checksum"]) and not _content_on_gpu() and \
+            os.environ.get("LZ4M_FRAME_FOLLOW", "1") != "0"
+        r = _decode_records(d_frame, info, nb, rec_pos[:nb], rec_len[:nb], rec_raw[:nb].to(torch.bool), crc_pos,
+                            follow_hash=follow)
+        out_t, total, first_err = r[:3]
+        got = r[3] if follow else None
     _frame_errors(first_err, ("end", _end, cpos if cpos >= 0 else None), info, total)
     if info["content_checksum"]:
         want = int(_le32_at(d_frame, torch.tensor([cpos], dtype=torch.int64, device=dev)).item()) & 0xFFFFFFFF
-        got = _xxh32_dev(out_t, total) if total else _xxh32_dev(b"")
+        if got is None:
+            got = _xxh32_dev(out_t, total) if total else _xxh32_dev(b"")
         if got != want:
             raise _err("LZ4F_decompress", "contentChecksum_invalid")
     if not total:
@@ -483,11 +488,30 @@ def _frame_errors(first_err, state, info, total):
         raise RuntimeError(f"Frame incomplete. LZ4F_decompress returned: {state[1]}")
 
 
-def _decode_records(d_frame, info, nb, c_off, c_len, raw_mask, crc_pos):
+_FOLLOW_CHUNKS = 8   # block-ordered decode launches the content hash follows
+
+
+def _decode_records(d_frame, info, nb, c_off, c_len, raw_mask, crc_pos, follow_hash=False):
     """Decode nb block records of a frame in device memory: payload at
     c_off[i] (int64), stored size c_len[i] (int32), raw_mask[i] = stored
     uncompressed, crc_pos[i] = position of its LE32 block checksum or -1.
-    Returns (out tensor, total decoded bytes, first error or None)."""
+    Returns (out tensor, total decoded bytes, first error or None), and with
+    ``follow_hash`` a fourth item: the content XXH32 of the output, or None
+    when the caller must hash it.
+
+    ``follow_hash`` (independent blocks, no stored ones): the blocks decode
+    in _FOLLOW_CHUNKS launches in block order, and a host thread hashes each
+    launch's output as soon as it is done (lz4frame.c:1849-1850 hashes the
+    output in order), reading it from the decode slots on the assumption
+    that every block but the last decodes to the full block size (what
+    LZ4F_compressFrame writes), so the slots are the output.  The assumption
+    is checked once the decode is done; if it fails, the hash is discarded
+    and the output gathered and hashed as before."""
+    if follow_hash:
+        r = _decode_records_follow(d_frame, info, nb, c_off, c_len, raw_mask, crc_pos)
+        if r is not None:
+            return r
+        return _decode_records(d_frame, info, nb, c_off, c_len, raw_mask, crc_pos) + (None,)
     dev = d_frame.device
     maxb = info["block_size"]
     status = torch.empty(nb, dtype=torch.int32, device=dev)
@@ -527,6 +551,53 @@ def _decode_records(d_frame, info, nb, c_off, c_len, raw_mask, crc_pos):
     if sel_r.numel():                                          # raw blocks straight from the frame
         N.gather(d_frame, c_off[sel_r], lens[sel_r], out_t, offs[sel_r], sel_r.numel())
     return out_t, total, None
+
+
+def _decode_records_follow(d_frame, info, nb, c_off, c_len, raw_mask, crc_pos):
+    """_decode_records(follow_hash=True) for frames it applies to, else None."""
+    if info["block_linked"] or nb < 2 * _FOLLOW_CHUNKS or bool(raw_mask.any()):
+        return None
+    dev = d_frame.device
+    maxb = info["block_size"]
+    status = torch.empty(nb, dtype=torch.int32, device=dev)
+    crc_bad = None
+    if info["block_checksum"]:
+        sums = torch.empty(nb, dtype=torch.int32, device=dev)
+        N.launch_xxh32_batch(d_frame, c_off, c_len.to(torch.int64), 0, sums, nb)
+        crc_bad = (sums.to(torch.int64) & 0xFFFFFFFF) != _le32_at(d_frame, crc_pos)
+    slots = torch.empty(nb * maxb + 16, dtype=torch.uint8, device=dev)
+    slot_off = torch.arange(nb, dtype=torch.int64, device=dev) * maxb
+    caps = torch.full((nb,), maxb, dtype=torch.int32, device=dev)
+    bounds = [nb * k // _FOLLOW_CHUNKS for k in range(_FOLLOW_CHUNKS + 1)]
+    spans = []
+    for k in range(_FOLLOW_CHUNKS):
+        lo, hi = bounds[k], bounds[k + 1]
+        N.launch_decompress(d_frame, c_off[lo:hi], c_len[lo:hi], slots, slot_off[lo:hi], caps[lo:hi],
+                            status[lo:hi], hi - lo)
+        ev = torch.cuda.Event()
+        ev.record()
+        # full blocks only: the last block's size is known after the decode
+        spans.append((lo * maxb, min(hi, nb - 1) * maxb, ev))
+    hasher = _HashThread(lambda: N.xxh32_of_device_spans(slots, spans))
+    hasher.start()
+    try:
+        bad = status < 0
+        if crc_bad is not None:
+            bad = bad | crc_bad
+        if bool(bad.any()):
+            i = int(torch.nonzero(bad).flatten()[0])
+            code = "blockChecksum_invalid" if crc_bad is not None and bool(crc_bad[i]) else "decompressionFailed"
+            return None, 0, (i, code), None
+        st = status.cpu()
+        full = bool((st[: nb - 1] == maxb).all())
+    finally:
+        hasher.join()
+    if not full:
+        return None
+    total = (nb - 1) * maxb + int(st[nb - 1])
+    state = hasher.result()
+    state = N.xxh32_of_device_spans(slots, [((nb - 1) * maxb, total, None)], state=state)
+    return slots, total, None, state.digest()
 
 
 def _decode_linked(d_frame, c_off, c_len, raw_mask, out, status, maxb):

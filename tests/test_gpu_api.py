@@ -578,6 +578,56 @@ def test_frame_device_roundtrip_large_blocks(gpu):
         assert torch.equal(out, d)
 
 
+@pytest.mark.parametrize("block_checksum", [False, True])
+def test_frame_decompress_device_hash_follows_decode(gpu, block_checksum):
+    """Frames of >= 16 independent blocks with a content checksum decode in
+    block-ordered launches that a host thread hashes as they finish
+    (decompress_device's follow path, on the assumption that every block but
+    the last is full): full frames, a corrupted content checksum, a corrupted
+    block checksum, and a hand-made frame with a short block mid-frame (the
+    assumption fails: the output is gathered and hashed as before)."""
+    import struct
+    import torch
+    from lz4 import _synth
+    from lz4 import _native as N
+    from lz4.frame._frame import _header
+    # text: every block compresses (a stored block sends the frame down the plain path)
+    data = _synth.blocks(40, "text", seed=31).tobytes() + b"tail" * 333
+    c = lz4.frame.compress(data, block_size=lz4.frame.BLOCKSIZE_MAX64KB, block_linked=False,
+                           content_checksum=True, block_checksum=block_checksum)
+    out = lz4.frame.decompress_device(_dev(c, gpu))
+    assert torch.equal(out.cpu(), torch.frombuffer(bytearray(data), dtype=torch.uint8))
+    bad = bytearray(c)
+    bad[-2] ^= 0x10
+    with pytest.raises(RuntimeError, match="ERROR_contentChecksum_invalid"):
+        lz4.frame.decompress_device(_dev(bad, gpu))
+    if block_checksum:
+        bad = bytearray(c)
+        bad[7 + 4 + 20 * 65536 // 3] ^= 0x01   # inside an early block's payload
+        with pytest.raises(RuntimeError) as e:
+            lz4.frame.decompress_device(_dev(bad, gpu))
+        with pytest.raises(RuntimeError) as h:
+            lz4.frame.decompress(bytes(bad))
+        assert str(e.value) == str(h.value)
+    # a short compressed block in the middle of the frame (valid for LZ4F_decompress)
+    chunks = [data[i * 65536:(i + 1) * 65536] for i in range(20)]
+    chunks[9] = chunks[9][:1000]
+    chunks.append(b"x" * 65536)
+    body = b""
+    for ch in chunks:
+        blk = lz4.block.compress(ch, store_size=False)
+        assert len(blk) < len(ch)
+        body += struct.pack("<I", len(blk)) + blk
+        if block_checksum:
+            body += struct.pack("<I", N.xxh32_host(blk))
+    plain = b"".join(chunks)
+    frame = _header(4, False, block_checksum, 0, True) + body + struct.pack("<I", 0) + \
+        struct.pack("<I", N.xxh32_host(plain))
+    assert lz4.frame.decompress(frame) == plain
+    out = lz4.frame.decompress_device(_dev(frame, gpu))
+    assert out.cpu().numpy().tobytes() == plain
+
+
 def test_decompress_host_pipelined(gpu):
     """lz4.block.decompress_host: host-resident compressed blocks decoded in
     pipelined chunks into host memory; statuses and bytes equal the
