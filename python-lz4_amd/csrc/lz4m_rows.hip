@@ -973,7 +973,7 @@ __device__ __forceinline__ int32_t load_len(const uint8_t* dl, int32_t k, int32_
 // workgroup are independent (no barrier after the prologue); 256 shares the
 // put-mask and period tables (1.6 KB of LDS) between four waves.
 #ifndef LZ4M_ROWS_EWG
-#define LZ4M_ROWS_EWG 64
+#define LZ4M_ROWS_EWG 256
 #endif
 constexpr int kEWG = LZ4M_ROWS_EWG;
 static_assert(kEWG == 64 || kEWG == 256, "executor workgroup: 64 or 256 threads");

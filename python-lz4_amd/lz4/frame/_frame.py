@@ -581,6 +581,10 @@ def _decode_records_follow(d_frame, info, nb, c_off, c_len, raw_mask, crc_pos):
     hasher = _HashThread(lambda: N.xxh32_of_device_spans(slots, spans))
     hasher.start()
     try:
+        # wait for the decode on the last launch's event, which releases the
+        # GIL (a tensor read-back waits holding it, and the hash thread needs
+        # it between chunks: r05p measured no overlap that way)
+        spans[-1][2].synchronize()
         bad = status < 0
         if crc_bad is not None:
             bad = bad | crc_bad
