@@ -488,7 +488,7 @@ def _frame_errors(first_err, state, info, total):
         raise RuntimeError(f"Frame incomplete. LZ4F_decompress returned: {state[1]}")
 
 
-_FOLLOW_CHUNKS = 8   # block-ordered decode launches the content hash follows
+_FOLLOW_CHUNKS = 16   # block-ordered decode launches the content hash follows
 
 
 def _decode_records(d_frame, info, nb, c_off, c_len, raw_mask, crc_pos, follow_hash=False):
