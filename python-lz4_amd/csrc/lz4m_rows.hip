@@ -241,6 +241,20 @@ __device__ __forceinline__ uint32_t dword_at(u32x4 w, uint32_t k) {
     return __builtin_amdgcn_alignbyte(hi, lo, k & 3);
 }
 
+// the 4 bytes at k (0..28) of the 32-byte window a|b, the dwords selected by
+// a tree on the index bits
+__device__ __forceinline__ uint32_t dword32_tree(u32x4 a, u32x4 b, uint32_t k) {
+    const uint32_t q = k >> 2;
+    const bool q1 = (q & 1u) != 0, q2 = (q & 2u) != 0, q4 = (q & 4u) != 0;
+    // dword q: pairs (x, y), (z, w) of a and b by bit 0, then by bit 1, then bit 2
+    const uint32_t l0 = q1 ? a.y : a.x, l1 = q1 ? a.w : a.z, l2 = q1 ? b.y : b.x, l3 = q1 ? b.w : b.z;
+    const uint32_t lo = q4 ? (q2 ? l3 : l2) : (q2 ? l1 : l0);
+    // dword q + 1 (0 past the window)
+    const uint32_t h0 = q1 ? a.z : a.y, h1 = q1 ? b.x : a.w, h2 = q1 ? b.z : b.y, h3 = q1 ? 0u : b.w;
+    const uint32_t hi = q4 ? (q2 ? h3 : h2) : (q2 ? h1 : h0);
+    return __builtin_amdgcn_alignbyte(hi, lo, k & 3);
+}
+
 // the 4 bytes at k (0..28) of the 32-byte window a|b
 __device__ __forceinline__ uint32_t dword32(u32x4 a, u32x4 b, uint32_t k) {
     const uint32_t q = k >> 2;
@@ -719,6 +733,12 @@ constexpr int32_t kRowsH = LZ4M_ROWS_H;
 #define LZ4M_ROWS_ORDER 1   // 1 (required: FarSrc is shared by P and Q): parse ahead after this round's passes
 #endif
 static_assert(LZ4M_ROWS_ORDER == 1, "the far-source pieces (FarSrc) are reused by the round parsed ahead");
+#ifndef LZ4M_ROWS_FARXS
+#define LZ4M_ROWS_FARXS 0   // far sources read back from the lane's literal slot (A/B)
+#endif
+#ifndef LZ4M_ROWS_OFFTREE
+#define LZ4M_ROWS_OFFTREE 1   // the offset's dword pair by a select tree (r05v A/B)
+#endif
 #ifndef LZ4M_ROWS_OFFLDS
 // 1: the match offset read back from the literal's LDS slot (72 VALU fewer
 // in the kernel).  r05q: the first rows test ended in an illegal memory
@@ -838,6 +858,13 @@ __device__ __forceinline__ void parse_round(PSeq& P, int32_t jj, int32_t r, int3
     const uint32_t q0 = lq >> 2, q1 = q0 < 7u ? q0 + 1u : 7u;   // (lq = 28: one dword, shift 0)
     const uint32_t dwo = __builtin_amdgcn_alignbyte(xd[q1], xd[q0], lq & 3u);
     const uint32_t bsh = 8u * ((uint32_t)lit - lq);
+#elif LZ4M_ROWS_OFFTREE
+    // the dword pair at pq selected by a tree on its three index bits (14
+    // selects) for every lane, instead of a 16-byte and a 32-byte select chain
+    // both computed and selected between
+    const uint32_t pq = (uint32_t)(po < 28 ? po : 28);
+    const uint32_t dwo = dword32_tree(wa, wb, pq);
+    const uint32_t bsh = 8u * ((uint32_t)po - pq);
 #else
     const uint32_t pq = (uint32_t)(po < 28 ? po : 28);
     const uint32_t dwo = lit <= 12 ? window_dword(wa, (uint32_t)po) : dword32(wa, wb, pq);
@@ -1205,11 +1232,24 @@ __global__ __launch_bounds__(kEWG) __attribute__((amdgpu_waves_per_eu(LZ4M_ROWS_
                                     (5ull << 33) | (4ull << 36) | (3ull << 39) | (2ull << 42) | (1ull << 45);
         const int32_t stp = per ? 16 - (int32_t)((kRem16 >> (3u * ((uint32_t)off & 15u))) & 7u) : 16;
         bool pend = u;
+#if LZ4M_ROWS_FARXS
+        // a far source's two pieces wait in the lane's literal slot (the
+        // literals are placed; the next round's parse refills the slot after
+        // the passes), so that a copy reads every source from LDS by address
+        if (far) XSL[0] = g0;
+        if (far & !late & (ml > 16)) XSL[1] = g1;
+        const lds_u8* const farp = (const lds_u8*)XSL;
+#endif
 #if LZ4M_ROWS_PUTMASK >= 3
         // one match copy (exec-masked to the ready lanes: an LDS access costs per active lane)
         auto copy_match = [&]() __attribute__((always_inline)) {
+#if LZ4M_ROWS_FARXS
+            const u32x4 l0 = lds_ld16u(far ? farp : HB + (s0 >= base ? s0 - base : 0));
+            u32x4 v0 = l0;
+#else
             const u32x4 l0 = (LZ4M_ROWS_XP & 2048) ? u32x4{(uint32_t)s0, 0u, 0u, 0u} : lds_ld16u(HB + (s0 >= base ? s0 - base : 0));
             u32x4 v0 = far ? g0 : l0;
+#endif
             if (per) v0 = period_perm(l0, PS + 8 * off);
             if (!(LZ4M_ROWS_XP & 1024)) LDS_PUT(HB + (m - base), v0, ml);
             if (ml > stp && !(LZ4M_ROWS_XP & 512)) {   // the rest (matches longer than one step)
@@ -1222,10 +1262,16 @@ __global__ __launch_bounds__(kEWG) __attribute__((amdgpu_waves_per_eu(LZ4M_ROWS_
                         // with the first; later pieces are loaded now, only where
                         // some lane needs one (this wait then covers only loads
                         // older than the round's own requests, LZ4M_ROWS_ORDER)
+#if LZ4M_ROWS_FARXS
+                        const bool pc1 = (i == 16) & far & !late;
+                        v = lds_ld16u((sp < base) & pc1 ? farp + 16 : HB + (sp >= base ? sp - base : 0));
+                        {
+#else
                         v = (LZ4M_ROWS_XP & 2048) ? u32x4{(uint32_t)sp, 0u, 0u, 0u} : lds_ld16u(HB + (sp >= base ? sp - base : 0));
                         if (!(LZ4M_ROWS_XP & 2)) {
                             const bool pc1 = (i == 16) & far & !late;
                             if (sp < base && pc1) v = g1;
+#endif
                             const bool hb = (sp < base) & !pc1;
                             if (__any(hb)) {
                                 const u32x4 x = ld16(d + (hb ? sp : 0));
