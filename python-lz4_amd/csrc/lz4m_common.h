@@ -115,6 +115,9 @@ __device__ __forceinline__ u32x4 period_pattern(u32x4 w, uint32_t off) {
 #ifndef LZ4M_LDS_SKIP
 #define LZ4M_LDS_SKIP 0    // A/B: the last two masked ORs of a put only where some lane needs them
 #endif
+#ifndef LZ4M_LDS_MASKLANES
+#define LZ4M_LDS_MASKLANES 0   // A/B: a put's dwords 1-4 exec-masked to the lanes that reach them
+#endif
 #ifndef LZ4M_LDS_ALIGN
 #define LZ4M_LDS_ALIGN 1   // 0 = plain (unaligned) wide accesses; 2 = plain stores for wholly covered dwords
 #endif
@@ -198,12 +201,21 @@ __device__ __forceinline__ void lds_put_al(lds_u8* p, u32x4 v, int32_t k, lds_cu
         const uint32_t d3 = __builtin_amdgcn_perm(v.w, v.z, sel(m.w));
         const uint32_t d4 = __builtin_amdgcn_perm(0u, v.w, sel(m4));
         asm volatile("ds_mskor_b32 %0, %1, %2 offset:0" ::"v"(b4), "v"(m.x), "v"(d0) : "memory");
+#if LZ4M_LDS_MASKLANES
+        // dwords 1-4 only in the lanes whose put reaches them (an LDS access
+        // costs per active lane)
+        if (m.y) asm volatile("ds_mskor_b32 %0, %1, %2 offset:4" ::"v"(b4), "v"(m.y), "v"(d1) : "memory");
+        if (m.z) asm volatile("ds_mskor_b32 %0, %1, %2 offset:8" ::"v"(b4), "v"(m.z), "v"(d2) : "memory");
+        if (m.w) asm volatile("ds_mskor_b32 %0, %1, %2 offset:12" ::"v"(b4), "v"(m.w), "v"(d3) : "memory");
+        if (m4) asm volatile("ds_mskor_b32 %0, %1, %2 offset:16" ::"v"(b4), "v"(m4), "v"(d4) : "memory");
+#else
         asm volatile("ds_mskor_b32 %0, %1, %2 offset:4" ::"v"(b4), "v"(m.y), "v"(d1) : "memory");
         asm volatile("ds_mskor_b32 %0, %1, %2 offset:8" ::"v"(b4), "v"(m.z), "v"(d2) : "memory");
         if (!LZ4M_LDS_SKIP || __any(m.w != 0u))
             asm volatile("ds_mskor_b32 %0, %1, %2 offset:12" ::"v"(b4), "v"(m.w), "v"(d3) : "memory");
         if (!LZ4M_LDS_SKIP || __any(m4 != 0u))
             asm volatile("ds_mskor_b32 %0, %1, %2 offset:16" ::"v"(b4), "v"(m4), "v"(d4) : "memory");
+#endif
         return;
     }
 #endif
