@@ -116,7 +116,7 @@ __device__ __forceinline__ u32x4 period_pattern(u32x4 w, uint32_t off) {
 #define LZ4M_LDS_SKIP 0    // A/B: the last two masked ORs of a put only where some lane needs them
 #endif
 #ifndef LZ4M_LDS_MASKLANES
-#define LZ4M_LDS_MASKLANES 0   // A/B: a put's dwords 1-4 exec-masked to the lanes that reach them
+#define LZ4M_LDS_MASKLANES 0   // A/B: a put's dwords 1-4 exec-masked to the lanes that reach them (r05x: 0.8 % slower)
 #endif
 #ifndef LZ4M_LDS_ALIGN
 #define LZ4M_LDS_ALIGN 1   // 0 = plain (unaligned) wide accesses; 2 = plain stores for wholly covered dwords
