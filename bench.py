@@ -204,6 +204,31 @@ def cpu_baseline(host_blocks: np.ndarray, comp_host: list, seconds: float = 10.0
     return res
 
 
+def frame_cpu_reference(sample: bytes) -> dict | None:
+    """The reference's own LZ4F_compressFrame / LZ4F_decompress (oracle/_ref,
+    compiled from /root/reference/lz4libs) on ONE host thread over a sample of
+    config 4's input: 4 MiB independent blocks, content checksum, level 0 --
+    the rate the drop-in lz4.frame calls replace.  None when
+    the reference build is absent."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O   # test/bench infrastructure only
+    if not os.path.exists(O.REF_SO):
+        return None
+    ref = O.Reference()
+    t = time.perf_counter()
+    fr = ref.compress_frame(sample, block_size_id=7, linked=False, content_checksum=True)
+    tc = time.perf_counter() - t
+    dst = np.empty(len(sample) + 64, dtype=np.uint8)
+    t = time.perf_counter()
+    got = ref.decompress_frame_into(fr, dst)
+    td = time.perf_counter() - t
+    assert got == len(sample) and dst[:got].tobytes() == sample, "reference frame round trip failed"
+    return {"compress_gib_s": round(len(sample) / tc / GIB, 3), "decompress_gib_s": round(len(sample) / td / GIB, 3),
+            "threads": 1, "kind": "reference", "ratio": round(len(sample) / len(fr), 4),
+            "sample": f"LZ4F_compressFrame / LZ4F_decompress, first {len(sample) >> 20} MiB of the config-4 input, "
+                      "4 MiB independent blocks, content checksum, one call each on one thread"}
+
+
 def config5(src, n, world, rank, dev, wave_blocks, waves, strong_total):
     """BASELINE config 5: 256 M x 64 KiB = 16 TiB cannot be
     device-resident, so every rank compresses its share in waves of
@@ -657,12 +682,15 @@ def main():
             extra["frame4m"]["dropin_note"] = ("lz4.frame.compress(bytes, block_size=BLOCKSIZE_MAX4MB, block_linked=False, "
                                                "content_checksum=True) and lz4.frame.decompress of its result: host bytes "
                                                "in and out, exact parse, PCIe and the serial content XXH32 included")
+            if runs_cpu_baseline(rank, args.no_cpu):
+                extra["frame4m"]["cpu_reference"] = frame_cpu_reference(hb[: 1 << 30])
             del hb, fr_h
         # lz4.frame.compress's defaults (64 KiB linked blocks, the exact parse, byte-identical to the
         # reference): speculative-parallel linked compression on a 256 MiB sample of the same input
         LS = min(L, 256 << 20)
         dl = {}
-        dl_wall, _ = time_kernel(lambda: dl.__setitem__("f", _compress_frame(fsrc, LS)), 1, 1, world)
+        dl_wall, _ = time_kernel(lambda: dl.__setitem__("f", _compress_frame(fsrc, LS)), 3, 1, world)
+        dl_wall /= 3
         dfr = dl.pop("f")[0]
         assert torch.equal(F.decompress_device(dfr), fsrc[:LS]), "default linked frame does not round-trip"
         extra["frame4m"]["compress_frame_default_linked_gib_s"] = round(world * LS / dl_wall / GIB, 3)

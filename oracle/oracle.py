@@ -262,6 +262,39 @@ class Reference:
         return dst[:r].tobytes()
 
 
+    def decompress_frame_into(self, data, dst: np.ndarray) -> int:
+        """LZ4F_decompress of one whole frame into dst (large enough for the
+        content) in one call sequence (lz4frame.c:1556-2058); returns the
+        bytes written (bench's frame CPU reference; errors raise)."""
+        lib = self.lib
+        vp, sz = C.c_void_p, C.c_size_t
+        lib.LZ4F_createDecompressionContext.argtypes = [C.POINTER(vp), C.c_uint]
+        lib.LZ4F_createDecompressionContext.restype = sz
+        lib.LZ4F_freeDecompressionContext.argtypes = [vp]
+        lib.LZ4F_decompress.argtypes = [vp, vp, C.POINTER(sz), vp, C.POINTER(sz), vp]
+        lib.LZ4F_decompress.restype = sz
+        src, sp = _buf(data)
+        ctx = vp()
+        lib.LZ4F_createDecompressionContext(C.byref(ctx), 100)
+        pos = out = 0
+        try:
+            while True:
+                dsz = sz(dst.size - out)
+                ssz = sz(src.size - pos)
+                r = lib.LZ4F_decompress(ctx, dst.ctypes.data + out, C.byref(dsz), src.ctypes.data + pos,
+                                        C.byref(ssz), None)
+                out += dsz.value
+                pos += ssz.value
+                if lib.LZ4F_isError(r):
+                    raise RuntimeError("LZ4F_decompress failed")
+                if r == 0:
+                    return out
+                if dsz.value == 0 and ssz.value == 0:
+                    raise RuntimeError("LZ4F_decompress made no progress")
+        finally:
+            lib.LZ4F_freeDecompressionContext(ctx)
+
+
 class CpuBench:
     """Throughput harness over the reference build (kind 'reference') or the
     restatement (kind 'port')."""

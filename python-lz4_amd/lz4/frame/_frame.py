@@ -33,6 +33,7 @@ from __future__ import annotations
 import os
 import struct
 import threading
+import time
 
 import torch
 
@@ -377,6 +378,10 @@ def decompress(data, return_bytearray=False, return_bytes_read=False):
         out = bytearray() if return_bytearray else b""
         return (out, end) if return_bytes_read else out
     recs, state = _scan_blocks(mv, hsize, info)
+    if os.environ.get("LZ4M_FRAME_PIPELINE", "1") != "0":
+        r = _decompress_pipelined(mv, info, recs, state, bool(return_bytearray))
+        if r is not None:
+            return (r, state[1]) if return_bytes_read else r
     dev = N.device()
     nb = len(recs)
     out_t, total, first_err = None, 0, None
@@ -402,6 +407,189 @@ def decompress(data, return_bytearray=False, return_bytes_read=False):
             raise _err("LZ4F_decompress", "contentChecksum_invalid")
     if return_bytes_read:
         return out, bytes_read
+    return out
+
+
+class _FeedHash(threading.Thread):
+    """The content XXH32 on a host core, over host ranges handed to it in
+    order (put(ptr, n); put(None) ends it)."""
+
+    def __init__(self):
+        super().__init__(daemon=True)
+        import queue
+        self.q = queue.SimpleQueue()
+        self.st = N.HostXXH32(0)
+        self.error = None
+
+    def put(self, ptr, n=0):
+        self.q.put(None if ptr is None else (ptr, n))
+
+    def run(self):
+        try:
+            while True:
+                item = self.q.get()
+                if item is None:
+                    return
+                self.st.update_ptr(*item)
+        except BaseException as e:   # re-raised in the caller
+            self.error = e
+
+    def digest(self) -> int:
+        self.put(None)
+        self.join()
+        if self.error is not None:
+            raise self.error
+        return self.st.digest()
+
+
+def _decompress_pipelined(mv, info, recs, state, as_bytearray):
+    """``decompress`` of a large well-formed frame of independent compressed
+    blocks with a stored content size, as one pipeline: the frame goes to the
+    device in 64 MiB chunks, the blocks decode in three block-ordered launches
+    as their bytes land, the output comes back in 64 MiB chunks as
+    their launch ends -- straight into the result bytes -- and a host core
+    hashes the result behind the copies (the content checksum, lz4frame.c:1850,
+    one serial stream: the bound).  The stages that ran one after another
+    (upload, decode, download + hash) overlap.
+
+    Every block but the last is taken to decode to the full block size (what
+    LZ4F_compressFrame writes), so the slots are the output; this, the
+    statuses and the block checksums are checked at the end, and on any
+    mismatch this returns None and the caller decodes the frame the
+    sequential way (which raises the reference's exact error).  Also None
+    when the frame does not qualify.
+
+    A launch takes about one block's decode time whatever its size (one
+    wavefront per block; a 4 MiB block ~51 ms, profiles/r05/r05y), so the
+    launches are few and growing -- 1/16, 3/16, 12/16 of the blocks -- and
+    the first two run on two streams side by side: the first output is ready
+    one block-decode after 1/16 of the frame has landed, and the rest stays
+    ahead of the hash."""
+    nb = len(recs)
+    maxb = info["block_size"]
+    total = info["content_size"]
+    n = mv.nbytes
+    if (state[0] != "end" or info["block_linked"] or nb < 32 or n < N._BIG
+            or not total or not ((nb - 1) * maxb < total <= nb * maxb) or _content_on_gpu()
+            or any(r[0] for r in recs)):
+        return None
+    dev = N.device()
+    main = torch.cuda.current_stream(dev)
+    up = torch.cuda.Stream(dev, priority=-1)
+    down = torch.cuda.Stream(dev, priority=-1)
+    side = torch.cuda.Stream(dev)          # the second decode stream
+    crc = info["block_checksum"]
+    c_off = torch.tensor([r[1] for r in recs], dtype=torch.int64, device=dev)
+    c_len = torch.tensor([r[2] for r in recs], dtype=torch.int32, device=dev)
+    status = torch.empty(nb, dtype=torch.int32, device=dev)
+    sums = torch.empty(nb, dtype=torch.int32, device=dev) if crc else None
+    slots = torch.empty(nb * maxb + 16, dtype=torch.uint8, device=dev)
+    slot_off = torch.arange(nb, dtype=torch.int64, device=dev) * maxb
+    caps = torch.full((nb,), maxb, dtype=torch.int32, device=dev)
+    d_frame = torch.empty(n + 16, dtype=torch.uint8, device=dev)
+    d_frame[n:].zero_()
+    up.wait_stream(main)   # (after the allocations: their memory may be free only in main's order)
+    side.wait_stream(main)
+    C = N._CHUNK
+    thr = N._copy_threads()
+    src, _, keep = N._addr(mv)
+    out, dst = N._new_host_buffer(total, as_bytearray)
+    hasher = _FeedHash() if info["content_checksum"] else None
+    if hasher is not None:
+        hasher.start()
+    # spans: block-ordered decode launches; span k needs the frame up to ends[k]
+    bounds = [0, nb // 16, nb // 4, nb]
+    K = len(bounds) - 1
+    ends = [recs[bounds[k + 1] - 1][1] + recs[bounds[k + 1] - 1][2] + (4 if crc else 0) for k in range(K)]
+    span_ev = [None] * K
+    trace = [] if os.environ.get("LZ4M_PIPE_TRACE") else None
+    t0 = time.perf_counter()
+    fills = [(lo, min(n, lo + C)) for lo in range(0, n, C)]
+    drains = [(lo, min(total, lo + C)) for lo in range(0, total, C)]
+    # the span whose launch writes the last byte of each drain chunk
+    need = [next(k for k in range(K) if (b - 1) // maxb < bounds[k + 1]) for _, b in drains]
+    upb, downb = N._pinned_pair(C), N._pinned_pair(C)
+    up_ev, down_ev = [None, None], [torch.cuda.Event(), torch.cuda.Event()]
+    launched = 0
+    fi = di = dd = 0   # next fill, next drain to issue, next drain to finish
+    done = False
+    try:
+        while dd < len(drains):
+            # a download is queued only once its launch is done: a copy queued
+            # behind an event holds up the uploads (r05ac: the second launch
+            # waited for the first launch's end)
+            while di < len(drains) and di - dd < 2 and need[di] < launched and span_ev[need[di]].query():
+                lo, hi = drains[di]
+                with torch.cuda.stream(down):
+                    downb[di & 1][: hi - lo].copy_(slots[lo:hi], non_blocking=True)
+                    down_ev[di & 1].record(down)
+                di += 1
+            if dd < di and (fi == len(fills) or down_ev[dd & 1].query()):
+                lo, hi = drains[dd]
+                down_ev[dd & 1].synchronize()
+                N.lib().lz4m_host_copy(dst + lo, downb[dd & 1].data_ptr(), hi - lo, thr, None)
+                if hasher is not None:
+                    hasher.put(dst + lo, hi - lo)
+                if trace is not None:
+                    trace.append(("drain", dd, time.perf_counter() - t0))
+                dd += 1
+                continue
+            if fi < len(fills):   # upload the next frame chunk, launch the spans it completes
+                lo, hi = fills[fi]
+                b = upb[fi & 1]
+                if up_ev[fi & 1] is not None:
+                    up_ev[fi & 1].synchronize()
+                N.lib().lz4m_host_copy(b.data_ptr(), src + lo, hi - lo, thr, None)
+                with torch.cuda.stream(up):
+                    d_frame[lo:hi].copy_(b[: hi - lo], non_blocking=True)
+                    up_ev[fi & 1] = torch.cuda.Event()
+                    up_ev[fi & 1].record(up)
+                fi += 1
+                while launched < K and ends[launched] <= hi:
+                    k = launched
+                    st = side if k == 1 else main
+                    st.wait_event(up_ev[(fi - 1) & 1])
+                    a, z = bounds[k], bounds[k + 1]
+                    with torch.cuda.stream(st):
+                        if crc:
+                            N.launch_xxh32_batch(d_frame, c_off[a:z], c_len[a:z].to(torch.int64), 0, sums[a:z], z - a,
+                                                 stream=st)
+                        N.launch_decompress(d_frame, c_off[a:z], c_len[a:z], slots, slot_off[a:z], caps[a:z],
+                                            status[a:z], z - a, stream=st)
+                        span_ev[k] = torch.cuda.Event(enable_timing=trace is not None)
+                        span_ev[k].record(st)
+                    if trace is not None:
+                        trace.append(("launch", k, time.perf_counter() - t0))
+                    launched += 1
+                continue
+            if dd == di:   # everything uploaded and launched: wait for the next download's launch
+                span_ev[need[di]].synchronize()
+        done = True
+    finally:
+        if hasher is not None and not done:
+            hasher.put(None)
+        for e in up_ev + down_ev:
+            if e is not None:
+                e.synchronize()
+        N._pinned_release(C, upb)
+        N._pinned_release(C, downb)
+        del keep
+    got = hasher.digest() if hasher is not None else None
+    main.wait_stream(side)
+    if trace is not None:
+        import sys
+        trace.append(("hash", 0, time.perf_counter() - t0))
+        print("[lz4m] pipelined frame decode: " + " ".join(f"{a}{b}@{c * 1e3:.1f}" for a, b, c in trace
+                                                          if a != "drain" or b % 16 == 0 or b == len(drains) - 1),
+              file=sys.stderr, flush=True)
+    ok = (status[: nb - 1] == maxb).all() & (status[nb - 1] == total - (nb - 1) * maxb)
+    if crc:
+        crc_pos = torch.tensor([r[3] for r in recs], dtype=torch.int64, device=dev)
+        ok = ok & ((sums.to(torch.int64) & 0xFFFFFFFF) == _le32_at(d_frame, crc_pos)).all()
+    if not bool(ok):
+        return None
+    if info["content_checksum"] and got != struct.unpack_from("<I", mv, state[2])[0]:
+        raise _err("LZ4F_decompress", "contentChecksum_invalid")
     return out
 
 
@@ -488,7 +676,11 @@ def _frame_errors(first_err, state, info, total):
         raise RuntimeError(f"Frame incomplete. LZ4F_decompress returned: {state[1]}")
 
 
-_FOLLOW_CHUNKS = 16   # block-ordered decode launches the content hash follows
+# block-ordered decode launches the content hash follows (decompress_device).
+# A launch takes about one block's decode time whatever its size (4 MiB
+# blocks: ~51 ms, profiles/r05/r05y): 16 launches (826 ms) fell behind the
+# hash; 2, 4 and 8 launches measured 674-682 ms (r05y, r05ab)
+_FOLLOW_CHUNKS = 4
 
 
 def _decode_records(d_frame, info, nb, c_off, c_len, raw_mask, crc_pos, follow_hash=False):

@@ -628,6 +628,77 @@ def test_frame_decompress_device_hash_follows_decode(gpu, block_checksum):
     assert out.cpu().numpy().tobytes() == plain
 
 
+@pytest.mark.parametrize("block_checksum", [False, True])
+def test_frame_decompress_pipelined(gpu, monkeypatch, block_checksum):
+    """lz4.frame.decompress of a large frame of independent blocks with a
+    stored content size runs as one pipeline (upload chunks, block-ordered
+    decode launches, download chunks into the result, the content hash
+    behind them; _decompress_pipelined), here with the size thresholds and
+    the chunk shrunk so a small frame takes many chunks: full frames (bytes,
+    bytearray, bytes_read), a corrupted content checksum, a corrupted block
+    checksum and a short block mid-frame (both: the pipeline's result is
+    discarded and the sequential path gives the reference's result or
+    error), and frames that do not qualify (no stored size, linked)."""
+    import struct
+    from lz4 import _synth
+    from lz4 import _native as N
+    from lz4.frame import _frame as FR
+    monkeypatch.setattr(N, "_BIG", 1 << 16)
+    monkeypatch.setattr(N, "_CHUNK", 1 << 18)
+    ran = []
+    orig = FR._decompress_pipelined
+
+    def spy(*a):
+        r = orig(*a)
+        ran.append(r is not None)
+        return r
+
+    monkeypatch.setattr(FR, "_decompress_pipelined", spy)
+    data = _synth.blocks(40, "text", seed=32).tobytes() + b"tail" * 333
+    kw = dict(block_size=lz4.frame.BLOCKSIZE_MAX64KB, block_linked=False, content_checksum=True,
+              block_checksum=block_checksum)
+    c = lz4.frame.compress(data, **kw)
+    assert lz4.frame.decompress(c) == data and ran == [True]
+    out, nread = lz4.frame.decompress(c + b"trailing", return_bytearray=True, return_bytes_read=True)
+    assert isinstance(out, bytearray) and out == data and nread == len(c) and ran[-1]
+    bad = bytearray(c)
+    bad[-2] ^= 0x10
+    with pytest.raises(RuntimeError, match="ERROR_contentChecksum_invalid"):
+        lz4.frame.decompress(bytes(bad))
+    if block_checksum:
+        bad = bytearray(c)
+        bad[7 + 8 + 4 + 20 * 65536 // 3] ^= 0x01   # inside an early block's payload
+        with pytest.raises(RuntimeError) as e:
+            lz4.frame.decompress(bytes(bad))
+        assert not ran[-1]
+        monkeypatch.setenv("LZ4M_FRAME_PIPELINE", "0")
+        with pytest.raises(RuntimeError) as h:
+            lz4.frame.decompress(bytes(bad))
+        monkeypatch.delenv("LZ4M_FRAME_PIPELINE")
+        assert str(e.value) == str(h.value)
+    # not qualifying: no stored content size, linked blocks
+    n0 = len(ran)
+    for extra in (dict(store_size=False), dict(block_linked=True)):
+        c2 = lz4.frame.compress(data, **{**kw, **extra})
+        assert lz4.frame.decompress(c2) == data
+    assert not any(ran[n0:])
+    # a short compressed block mid-frame, the stored size right: decoded, found
+    # not full, and redone the sequential way
+    chunks = [data[i * 65536:(i + 1) * 65536] for i in range(40)]
+    chunks[9] = chunks[9][:1000]
+    body = b""
+    for ch in chunks:
+        blk = lz4.block.compress(ch, store_size=False)
+        assert len(blk) < len(ch)
+        body += struct.pack("<I", len(blk)) + blk
+        if block_checksum:
+            body += struct.pack("<I", N.xxh32_host(blk))
+    plain = b"".join(chunks)
+    frame = FR._header(4, False, block_checksum, len(plain), True) + body + struct.pack("<I", 0) + \
+        struct.pack("<I", N.xxh32_host(plain))
+    assert lz4.frame.decompress(frame) == plain and not ran[-1]
+
+
 def test_decompress_host_pipelined(gpu):
     """lz4.block.decompress_host: host-resident compressed blocks decoded in
     pipelined chunks into host memory; statuses and bytes equal the

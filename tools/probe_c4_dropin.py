@@ -1,6 +1,6 @@
 """Dev probe: the drop-in config-4 calls on host bytes -- lz4.frame.compress
 (4 MiB independent blocks, content checksum, exact parse) and
-lz4.frame.decompress of its result -- with a stage split.  env: GIB (8)."""
+lz4.frame.decompress of its result (pipelined, and LZ4M_FRAME_PIPELINE=0) -- with a stage split.  env: GIB (8)."""
 import os
 import sys
 import time
@@ -22,6 +22,15 @@ hb = src.cpu().numpy().tobytes()
 print(f"host bytes ready ({time.perf_counter() - t0:.2f}s)", flush=True)
 kw = dict(block_size=F.BLOCKSIZE_MAX4MB, block_linked=False, content_checksum=True)
 F.decompress(F.compress(hb[: 64 << 20], **kw))
+from lz4.frame._frame import _compress_frame  # noqa: E402
+for rep in range(2):   # the device part alone: exact parse of 4 MiB independent blocks, no content checksum
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    fx, _ = _compress_frame(src.view(-1), L, content_checksum=False, block_size=7, block_linked=False, parse="exact")
+    torch.cuda.synchronize()
+    print(f"device exact frame compress (no content checksum): {L / (time.perf_counter() - t0) / 2**30:.2f} GiB/s",
+          flush=True)
+    del fx
 for rep in range(2):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -34,6 +43,15 @@ for rep in range(2):
     t3 = time.perf_counter()
     ok = out == hb
     t4 = time.perf_counter()
+    del out
+    os.environ["LZ4M_FRAME_PIPELINE"] = "0"
+    t5 = time.perf_counter()
+    out0 = F.decompress(fr)
+    t6 = time.perf_counter()
+    os.environ["LZ4M_FRAME_PIPELINE"] = "1"
+    print(f"  sequential decompress (LZ4M_FRAME_PIPELINE=0) {L / (t6 - t5) / 2**30:.2f} GiB/s, ok={out0 == hb}",
+          flush=True)
+    out = out0
     del d
     print(f"rep {rep}: to_device {L / (t1 - t0) / 2**30:.2f} GiB/s; compress {L / (t2 - t1) / 2**30:.2f} GiB/s "
           f"({t2 - t1:.2f}s, ratio {L / len(fr):.3f}); decompress {L / (t3 - t2) / 2**30:.2f} GiB/s ({t3 - t2:.2f}s); "

@@ -40,3 +40,16 @@ for kind in kinds:
                   + (f" passes={L.lz4m_compress_linked_passes()}" if name == "spec" else ""), flush=True)
         if "serial" in res:
             print("  same lengths:", bool(torch.equal(res["spec"][1], res["serial"][1])), flush=True)
+# the whole default-frame call as bench.py times it (frame records, emit, header) on the same bytes
+if os.environ.get("FRAME", "1") != "0":
+    from lz4.frame._frame import _compress_frame
+    data = _synth.blocks(mib * 16, kinds[0], seed=3)
+    d = torch.from_numpy(data.reshape(-1)).to(dev)
+    for rep in range(3):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        fr, _ = _compress_frame(d, d.numel())
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t
+        print(f"_compress_frame (64 KiB linked, exact): {dt * 1e3:.1f} ms {d.numel() / dt / 2**30:.3f} GiB/s "
+              f"passes={L.lz4m_compress_linked_passes()}", flush=True)
