@@ -10,9 +10,15 @@ mib = int(sys.argv[1]) if len(sys.argv) > 1 else 64
 kinds = sys.argv[2:] or ["silesia"]
 dev = torch.device("cuda", 0)
 L = N.lib()
+BENCH_DATA = os.environ.get("DATA") == "bench"   # bench.py's config-4 input (make_batch, seed 77)
 for kind in kinds:
-    data = _synth.blocks(mib * 16, kind, seed=3)
-    d = torch.from_numpy(data.reshape(-1)).to(dev)
+    if BENCH_DATA:
+        sys.path.insert(0, ".")
+        import bench as B
+        d = B.make_batch(mib * 16, 4096, kind, 77, dev)
+    else:
+        data = _synth.blocks(mib * 16, kind, seed=3)
+        d = torch.from_numpy(data.reshape(-1)).to(dev)
     n = d.numel()
     for bsize in [int(x) for x in os.environ.get("BSIZES", "65536,4194304").split(",")]:
         nb = (n + bsize - 1) // bsize
@@ -43,8 +49,9 @@ for kind in kinds:
 # the whole default-frame call as bench.py times it (frame records, emit, header) on the same bytes
 if os.environ.get("FRAME", "1") != "0":
     from lz4.frame._frame import _compress_frame
-    data = _synth.blocks(mib * 16, kinds[0], seed=3)
-    d = torch.from_numpy(data.reshape(-1)).to(dev)
+    if not BENCH_DATA:
+        data = _synth.blocks(mib * 16, kinds[0], seed=3)
+        d = torch.from_numpy(data.reshape(-1)).to(dev)
     for rep in range(3):
         torch.cuda.synchronize()
         t = time.perf_counter()
