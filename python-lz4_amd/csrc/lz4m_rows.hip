@@ -917,7 +917,7 @@ __device__ __forceinline__ void parse_round(PSeq& P, int32_t jj, int32_t r, int3
     } else {
         FS.g0 = ld16(d + (pf ? s0 : 0));
         // the second piece [s0 + 16, s0 + 32) is flushed too (not late: s0 + 32 <= F)
-        FS.g1 = ld16(d + (pf & (ml > 16) ? s0 + 16 : 0));
+        FS.g1 = ld16(d + ((pf & (ml > 16)) ? s0 + 16 : 0));
     }
 #if !LZ4M_ROWS_OFFLDS
     const uint32_t sh = (uint32_t)lp;

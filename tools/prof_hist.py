@@ -18,8 +18,8 @@ lib = N.lib()
 NAMES = ["restage", "walk", "parse+prefix+ok", "literals", "passes", "flush", "long-literal", "exact tail",
          "rounds", "passes#", "seqs#", "blocks#", "", "", "", "block setup"]
 for kind in os.environ.get("KINDS", "silesia,text").split(","):
-    nb, bs = int(os.environ.get("NB", "32768")), 65536
-    src = B.make_batch(nb, min(4096, nb), kind, 7, dev)
+    nb, bs = int(os.environ.get("NB", "32768")), int(os.environ.get("BS", "65536"))   # BS: block size
+    src = B.make_batch(nb * bs // 65536, min(4096, nb * bs // 65536), kind, 7, dev)
     so = torch.arange(nb, dtype=torch.int64, device=dev) * bs
     sl = torch.full((nb,), bs, dtype=torch.int32, device=dev)
     cap = ((bs + bs // 255 + 16 + 15) // 16) * 16
@@ -27,14 +27,18 @@ for kind in os.environ.get("KINDS", "silesia,text").split(","):
     scap = torch.full((nb,), cap, dtype=torch.int32, device=dev)
     slots = torch.empty(nb * cap, dtype=torch.uint8, device=dev)
     olen = torch.empty(nb, dtype=torch.int32, device=dev)
-    N.launch_compress(src, so, sl, slots, soff, scap, olen, nb, N.TABLE_U16_HASH4, 1)
+    N.launch_compress(src, so, sl, slots, soff, scap, olen, nb, N.TABLE_U16_HASH4 if bs <= 65536 else N.TABLE_AUTO, 1)
     dst = torch.zeros(nb * bs, dtype=torch.uint8, device=dev)
     st = torch.empty(nb, dtype=torch.int32, device=dev)
     buf = (C.c_ulonglong * 16)()
     torch.cuda.synchronize()
     lib.lz4m_hist_prof(buf, 1)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
     N.launch_decompress(slots, soff, olen, dst, so, sl, st, nb)
+    e1.record()
     torch.cuda.synchronize()
+    print(f"{kind}: launch {e0.elapsed_time(e1):.2f} ms", flush=True)
     lib.lz4m_hist_prof(buf, 1)
     ok = bool((st == bs).all()) and torch.equal(dst, src)
     v = list(buf)
