@@ -119,6 +119,21 @@ __device__ __forceinline__ int32_t wave_incl_sum(int32_t v) {
     return v;
 }
 
+// OR of v over the wave (uniform): inclusive prefix OR as wave_incl_sum, read at lane 63
+__device__ __forceinline__ uint32_t wave_or(uint32_t v) {
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);   // row_shr:1
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);   // row_shr:2
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);   // row_shr:4
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);   // row_shr:8
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);   // row_bcast:15 -> rows 1, 3
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);   // row_bcast:31 -> rows 2, 3
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
+#ifndef LZ4M_PC_SCAT
+#define LZ4M_PC_SCAT 0   // A/B: the encoder's sequence lookup by a DPP-reduced start mask instead of a bpermute binary search (r05aj: same output, 0.3-0.7 % slower -- issue-bound, not latency-bound)
+#endif
+
 // set bits of m in lanes below this one
 __device__ __forceinline__ int32_t count_below(uint64_t m) {
     return (int32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -170,7 +185,19 @@ __device__ __forceinline__ int32_t emit_seqs(const uint8_t* s, uint8_t* d, int32
     if (op + total > cap) return -1;
     for (int32_t t0 = 0; t0 < ptotal; t0 += 64) {
         const int32_t t = t0 + (int32_t)lane;
-        // last sequence k < ns with pbase_k <= t (pbase ascends with k),
+        // last sequence k < ns with pbase_k <= t (pbase ascends with k)
+#if LZ4M_PC_SCAT
+        // without LDS: the sequences starting inside (t0, t0 + 64) set their
+        // bit of a wave-wide mask (OR-reduced by DPP), and lane t counts the
+        // bits at or below it on top of the last sequence starting by t0
+        const int k0 = (int)__builtin_popcountll(__ballot((int)lane < ns && pbase <= t0)) - 1;
+        const int32_t dd = pbase - t0;
+        const bool inr = (int)lane < ns && dd > 0 && dd < 64;
+        const uint32_t mlo = wave_or(inr && dd < 32 ? 1u << (dd & 31) : 0u);
+        const uint32_t mhi = wave_or(inr && dd >= 32 ? 1u << (dd & 31) : 0u);
+        const uint32_t mine = ((lane < 32 ? mlo : mhi) >> (lane & 31)) & 1u;
+        const int sq4 = (k0 + (int)__builtin_amdgcn_mbcnt_hi(mhi, __builtin_amdgcn_mbcnt_lo(mlo, 0u)) + (int)mine) << 2;
+#else
         // searched in ds_bpermute byte-address units (4 k): each step's
         // address is the previous one plus an instruction offset
         int sq4 = 0;
@@ -180,6 +207,7 @@ __device__ __forceinline__ int32_t emit_seqs(const uint8_t* s, uint8_t* d, int32
             const int32_t pk = __builtin_amdgcn_ds_bpermute(k4, pbase);
             if (k4 < 4 * ns && pk <= t) sq4 = k4;
         }
+#endif
         const int32_t pb = __builtin_amdgcn_ds_bpermute(sq4, pbase), ob = __builtin_amdgcn_ds_bpermute(sq4, obase),
                       L = __builtin_amdgcn_ds_bpermute(sq4, lit), O = __builtin_amdgcn_ds_bpermute(sq4, off),
                       M = __builtin_amdgcn_ds_bpermute(sq4, ml), S = __builtin_amdgcn_ds_bpermute(sq4, lstart);
