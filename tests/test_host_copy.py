@@ -137,3 +137,34 @@ def test_host_copy_many_from_many_threads():
     for t in ts:
         t.join(timeout=120)
     assert not bad
+
+
+@pytest.mark.parametrize("as_bytearray", [False, True])
+@pytest.mark.parametrize("huge", ["1", "0"])
+def test_new_host_buffer_filled_by_copy(monkeypatch, as_bytearray, huge):
+    """_new_host_buffer (the drop-in results: uninitialised bytes / bytearray,
+    transparent huge pages asked for on its aligned interior unless
+    LZ4M_HUGEPAGES=0): the right type and size, and a pool copy into its
+    address lands in the object."""
+    import lz4._native as N
+    monkeypatch.setenv("LZ4M_HUGEPAGES", huge)
+    n = (9 << 20) + 5
+    src = np.random.default_rng(3).integers(0, 256, n, dtype=np.uint8)
+    obj, addr = N._new_host_buffer(n, as_bytearray)
+    assert isinstance(obj, bytearray if as_bytearray else bytes) and len(obj) == n
+    N.lib().lz4m_host_copy(addr, src.ctypes.data_as(C.c_void_p), n, 4, None)
+    assert obj == src.tobytes()
+
+
+def test_feed_hash_in_order(oracle):
+    """The pipelined frame decode's hash thread (_FeedHash): ranges handed to
+    it in order hash to the one-shot XXH32 of their concatenation."""
+    from lz4.frame._frame import _FeedHash
+    data = np.random.default_rng(5).integers(0, 256, (3 << 20) + 77, dtype=np.uint8)
+    h = _FeedHash()
+    h.start()
+    cuts = [0, 1, 4096, 70000, 1 << 20, (2 << 20) + 3, data.size]
+    base = data.ctypes.data
+    for a, b in zip(cuts, cuts[1:]):
+        h.put(base + a, b - a)
+    assert h.digest() == oracle.xxh32(data.tobytes(), 0)
