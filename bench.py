@@ -534,7 +534,7 @@ def main():
                                      "kernel": "default dispatch: row decoder (>= 32 768 blocks)"}
 
     # ---- extra: end to end from pinned host memory (PCIe-inclusive) ----
-    # lz4.block.decompress_host: chunks of 65 536 blocks pipelined over three
+    # lz4.block.decompress_host: chunks of 16 384 blocks pipelined over three
     # streams (copy in || decode || copy out)
     if args.e2e_blocks > 0:
         import lz4.block as LB
@@ -551,7 +551,7 @@ def main():
         box = {}
 
         def do_e2e():
-            box["st"] = LB.decompress_host(h_comp, h_coff, h_clen, h_out, h_ooff, h_ocap, chunk_blocks=65536)
+            box["st"] = LB.decompress_host(h_comp, h_coff, h_clen, h_out, h_ooff, h_ocap, chunk_blocks=16384)
 
         e_wall, _ = time_kernel(do_e2e, max(1, args.steps // 2), 1, world)
         assert bool((box.pop("st") == BLOCK).all()), "end-to-end decode failed"
@@ -559,7 +559,7 @@ def main():
             torch.equal(h_out[-4 * BLOCK:], src[(ne - 4) * BLOCK: ne * BLOCK].cpu())
         extra["end_to_end_host_gib_s"] = round(world * ne * BLOCK / (e_wall / max(1, args.steps // 2)) / GIB, 2)
         extra["end_to_end_blocks"] = ne
-        extra["end_to_end_note"] = "pinned host bytes -> H2D -> decode -> D2H, 65 536-block chunks pipelined"
+        extra["end_to_end_note"] = "pinned host bytes -> H2D -> decode -> D2H, 16 384-block chunks pipelined"
         del h_comp, h_out
 
     # ---- extra: incompressible (random) blocks ----

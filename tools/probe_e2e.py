@@ -1,5 +1,7 @@
-"""Dev probe: lz4.block.decompress_host (host -> H2D -> decode -> D2H)
-rates by chunk size on NB silesia-like blocks."""
+"""Dev probe: lz4.block.decompress_host end to end (pinned host bytes -> H2D ->
+decode -> D2H) on NB x 64 KiB silesia-like blocks, per chunk size, with the
+copies queued as their waits complete (default) or all up front
+(LZ4M_HOST_QUEUED=1)."""
 import os
 import sys
 import time
@@ -15,30 +17,29 @@ from lz4 import _native as N  # noqa: E402
 
 dev = torch.device("cuda", 0)
 n = int(os.environ.get("NB", 1 << 18))
-src = B.make_batch(n, min(4096, n), "silesia", 2026, dev)
+src = B.make_batch(n, 4096, "silesia", 2026, dev)
 so, sl, slots, soff, scap, olen = B.compress_all(src, n, 0, dev)
 N.launch_compress(src, so, sl, slots, soff, scap, olen, n, N.TABLE_U16_HASH4, 1)
-coff = torch.cumsum(olen.to(torch.int64), 0) - olen.to(torch.int64)
-tot = int(olen.to(torch.int64).sum())
-packed = torch.empty(tot, dtype=torch.uint8, device=dev)
-N.gather(slots, soff, olen, packed, coff, n)
+offs = N.exclusive_scan(olen)
+tot = int(offs[n])
+comp = torch.empty(tot, dtype=torch.uint8, device=dev)
+N.gather(slots, soff, olen, comp, offs, n)
+del slots
 h_comp = torch.empty(tot, dtype=torch.uint8, pin_memory=True)
-h_comp.copy_(packed)
+h_comp.copy_(comp)
 h_out = torch.empty(n * 65536, dtype=torch.uint8, pin_memory=True)
-h_coff, h_clen = coff.cpu(), olen.cpu()
+h_coff, h_clen = offs[:n].cpu(), olen.cpu()
 h_ooff = torch.arange(n, dtype=torch.int64) * 65536
 h_ocap = torch.full((n,), 65536, dtype=torch.int32)
-del slots, packed
-for how in ["engine"]:
-    for cb in [int(x) for x in os.environ.get("CHUNKS", "32768,65536,131072").split(",")]:
-        LB.decompress_host(h_comp, h_coff, h_clen, h_out, h_ooff, h_ocap, chunk_blocks=cb)
-        ts = []
-        for _ in range(2):
-            h_out.zero_()
+for mode in ("0", "1"):
+    os.environ["LZ4M_HOST_QUEUED"] = mode
+    for cb in (65536, 32768, 16384):
+        best = 1e9
+        for rep in range(3):
+            torch.cuda.synchronize()
             t = time.perf_counter()
             st = LB.decompress_host(h_comp, h_coff, h_clen, h_out, h_ooff, h_ocap, chunk_blocks=cb)
-            ts.append(time.perf_counter() - t)
-        ok = bool((st == 65536).all()) and torch.equal(h_out[-65536 * 8:].to(dev), src[-65536 * 8:]) \
-            and torch.equal(h_out[:65536 * 8].to(dev), src[:65536 * 8])
-        print(f"{how:6s} chunk {cb:6d}: {n * 65536 / min(ts) / 2**30:.2f} GiB/s  {'ok' if ok else 'FAILED'}",
-              flush=True)
+            torch.cuda.synchronize()
+            best = min(best, time.perf_counter() - t)
+        ok = bool((st == 65536).all()) and torch.equal(h_out[-65536:], src[-65536:].cpu())
+        print(f"queued={mode} chunk={cb}: {n * 65536 / best / 2**30:.2f} GiB/s ({best * 1e3:.1f} ms) ok={ok}", flush=True)
