@@ -568,7 +568,8 @@ def _decompress_pipelined(mv, info, recs, state, as_bytearray):
     finally:
         if hasher is not None and not done:
             hasher.put(None)
-        for e in up_ev + down_ev:
+        # (on an error too: no copy or launch may still use the buffers freed on return)
+        for e in up_ev + down_ev + span_ev:
             if e is not None:
                 e.synchronize()
         N._pinned_release(C, upb)
