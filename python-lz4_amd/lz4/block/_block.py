@@ -575,56 +575,61 @@ def decompress_host(comp: torch.Tensor, comp_off: torch.Tensor, comp_len: torch.
     s_in.wait_stream(cur)
     s_out.wait_stream(cur)
     s_dec.wait_stream(cur)
-    if os.environ.get("LZ4M_HOST_QUEUED") == "1":   # A/B: every copy queued up front behind its event
-        for i, (lo, hi) in enumerate(chunks):
-            b = i & 1
-            a0, a1 = span(c_off, c_len, lo, hi)
-            b0, b1 = span(o_off, o_cap, lo, hi)
-            with torch.cuda.stream(s_in):
-                if ev_free[b] is not None:
-                    s_in.wait_event(ev_free[b])                    # chunk i-2 has left buffer b
-                d_in[b][: a1 - a0].copy_(comp[a0:a1], non_blocking=True)
-                ev_in[b].record(s_in)
-            with torch.cuda.stream(s_dec):
-                s_dec.wait_event(ev_in[b])
-                N.launch_decompress(d_in[b], meta[0, lo:hi], lens[0, lo:hi], d_out[b], meta[1, lo:hi],
-                                    lens[1, lo:hi], status[lo:hi], hi - lo, s_dec)
-                ev_dec[b].record(s_dec)
-            with torch.cuda.stream(s_out):
-                s_out.wait_event(ev_dec[b])
-                out[b0:b1].copy_(d_out[b][: b1 - b0], non_blocking=True)
-                ev_free[b] = torch.cuda.Event()
-                ev_free[b].record(s_out)
-    else:
-        # Copies are queued only once what they wait for is done (the host
-        # waits on the event): a copy queued behind an event holds up the
-        # copies in the other direction on the copy engine (the upload of
-        # chunk i+1 waited for the decode of chunk i, r05ac/r05ad).
-        def issue_out(b, b0, b1):
-            ev_dec[b].synchronize()                                # its decode is done
-            with torch.cuda.stream(s_out):
-                out[b0:b1].copy_(d_out[b][: b1 - b0], non_blocking=True)
-                ev_free[b] = torch.cuda.Event()
-                ev_free[b].record(s_out)
+    try:
+        if os.environ.get("LZ4M_HOST_QUEUED") == "1":   # A/B: every copy queued up front behind its event
+            for i, (lo, hi) in enumerate(chunks):
+                b = i & 1
+                a0, a1 = span(c_off, c_len, lo, hi)
+                b0, b1 = span(o_off, o_cap, lo, hi)
+                with torch.cuda.stream(s_in):
+                    if ev_free[b] is not None:
+                        s_in.wait_event(ev_free[b])                    # chunk i-2 has left buffer b
+                    d_in[b][: a1 - a0].copy_(comp[a0:a1], non_blocking=True)
+                    ev_in[b].record(s_in)
+                with torch.cuda.stream(s_dec):
+                    s_dec.wait_event(ev_in[b])
+                    N.launch_decompress(d_in[b], meta[0, lo:hi], lens[0, lo:hi], d_out[b], meta[1, lo:hi],
+                                        lens[1, lo:hi], status[lo:hi], hi - lo, s_dec)
+                    ev_dec[b].record(s_dec)
+                with torch.cuda.stream(s_out):
+                    s_out.wait_event(ev_dec[b])
+                    out[b0:b1].copy_(d_out[b][: b1 - b0], non_blocking=True)
+                    ev_free[b] = torch.cuda.Event()
+                    ev_free[b].record(s_out)
+        else:
+            # Copies are queued only once what they wait for is done (the host
+            # waits on the event): a copy queued behind an event holds up the
+            # copies in the other direction on the copy engine (the upload of
+            # chunk i+1 waited for the decode of chunk i, r05ac/r05ad).
+            def issue_out(b, b0, b1):
+                ev_dec[b].synchronize()                                # its decode is done
+                with torch.cuda.stream(s_out):
+                    out[b0:b1].copy_(d_out[b][: b1 - b0], non_blocking=True)
+                    ev_free[b] = torch.cuda.Event()
+                    ev_free[b].record(s_out)
 
-        pending = None
-        for i, (lo, hi) in enumerate(chunks):
-            b = i & 1
-            a0, a1 = span(c_off, c_len, lo, hi)
-            if ev_free[b] is not None:
-                ev_free[b].synchronize()                           # chunk i-2 has left buffer b
-            with torch.cuda.stream(s_in):
-                d_in[b][: a1 - a0].copy_(comp[a0:a1], non_blocking=True)
-                ev_in[b].record(s_in)
-            with torch.cuda.stream(s_dec):
-                s_dec.wait_event(ev_in[b])
-                N.launch_decompress(d_in[b], meta[0, lo:hi], lens[0, lo:hi], d_out[b], meta[1, lo:hi],
-                                    lens[1, lo:hi], status[lo:hi], hi - lo, s_dec)
-                ev_dec[b].record(s_dec)
-            if pending is not None:
-                issue_out(*pending)
-            pending = (b,) + span(o_off, o_cap, lo, hi)
-        issue_out(*pending)
+            pending = None
+            for i, (lo, hi) in enumerate(chunks):
+                b = i & 1
+                a0, a1 = span(c_off, c_len, lo, hi)
+                if ev_free[b] is not None:
+                    ev_free[b].synchronize()                           # chunk i-2 has left buffer b
+                with torch.cuda.stream(s_in):
+                    d_in[b][: a1 - a0].copy_(comp[a0:a1], non_blocking=True)
+                    ev_in[b].record(s_in)
+                with torch.cuda.stream(s_dec):
+                    s_dec.wait_event(ev_in[b])
+                    N.launch_decompress(d_in[b], meta[0, lo:hi], lens[0, lo:hi], d_out[b], meta[1, lo:hi],
+                                        lens[1, lo:hi], status[lo:hi], hi - lo, s_dec)
+                    ev_dec[b].record(s_dec)
+                if pending is not None:
+                    issue_out(*pending)
+                pending = (b,) + span(o_off, o_cap, lo, hi)
+            issue_out(*pending)
+    finally:
+        # (on an error too: no copy or launch may still use the buffers freed on return)
+        for s_ in (s_in, s_dec, s_out):
+            s_.synchronize()
     cur.wait_stream(s_out)
     cur.wait_stream(s_dec)
     st = status.cpu()
