@@ -733,6 +733,12 @@ def _decode_records(d_frame, info, nb, c_off, c_len, raw_mask, crc_pos, follow_h
         return None, 0, (i, code)
     if linked:
         return slots, int(sizes.to(torch.int64).sum()), None
+    # no stored block and every block but the last full (what LZ4F_compressFrame
+    # writes): the slots already are the output, no gather (one read-back)
+    chk = torch.stack([(~raw_mask).all().to(torch.int64), (status[: nb - 1] == maxb).all().to(torch.int64),
+                       status[nb - 1].to(torch.int64)]).cpu()
+    if int(chk[0]) and int(chk[1]):
+        return slots, (nb - 1) * maxb + int(chk[2]), None
     lens = sizes.to(torch.int32)
     offs = N.exclusive_scan(lens)
     total = int(offs[-1].item())
