@@ -34,6 +34,8 @@
 // every step above is written to keep both the VALU and the per-CU scalar
 // unit short.
 #include "lz4m_common.h"
+
+#include <stdlib.h>
 #include "../../include/lz4m.h"
 
 namespace lz4m {
@@ -291,9 +293,18 @@ struct Chunk {
 #define LZ4M_PC_XCHG 0
 #endif
 
-template <bool BIG, int HB>
+// WIN (blocks > 64 KiB): the table holds the low 16 bits of each position
+// (u16, as for blocks <= 64 KiB) instead of whole u32 positions, and a
+// candidate is the most recent earlier position with those bits -- inside
+// the 64 KiB an offset can reach (lz4.c:1064).  An entry older than that
+// aliases to a position in the window; the 4-byte verify takes it only if its
+// bytes match, and then it is a valid match like any other.  Half the LDS of
+// the u32 table, so twice the waves per CU.
+template <bool BIG, int HB, bool WIN = false>
 __device__ __forceinline__ void chunk_issue(Chunk& C, const uint8_t* s, uint32_t* table32, int32_t p0, uint32_t v,
                                             int32_t N, int32_t mlast, uint32_t lane) {
+    constexpr bool U32 = BIG && !WIN;   // whole positions in a u32 table
+    static_assert(!(LZ4M_PC_XCHG && WIN), "the exchange variant has no windowed table");
     const int32_t p = p0 + (int32_t)lane;
     const bool act = p + 4 <= N;
     const uint32_t h = act ? phash<HB>(v) : (1u << HB);
@@ -323,11 +334,21 @@ __device__ __forceinline__ void chunk_issue(Chunk& C, const uint8_t* s, uint32_t
     const uint64_t earlier = eq & lt;
     const bool later = (eq >> lane) > 1u;
     uint16_t* table16 = reinterpret_cast<uint16_t*>(table32);
-    const uint32_t empty = BIG ? 0xFFFFFFFFu : kEmpty;
-    const uint32_t old = act ? (BIG ? table32[h] : (uint32_t)table16[h]) : empty;
-    const int32_t cand = earlier ? p0 + 63 - (int32_t)__builtin_clzll(earlier) : (old == empty ? -1 : (int32_t)old);
+    const uint32_t empty = U32 ? 0xFFFFFFFFu : kEmpty;
+    const uint32_t old = act ? (U32 ? table32[h] : (uint32_t)table16[h]) : empty;
+    int32_t cand;
+    if (earlier) {
+        cand = p0 + 63 - (int32_t)__builtin_clzll(earlier);
+    } else if (old == empty) {
+        cand = -1;
+    } else if (WIN) {   // the most recent earlier position with these low 16 bits (none at distance 0)
+        const int32_t dd = (p - (int32_t)old) & 0xFFFF;
+        cand = dd ? p - dd : -1;
+    } else {
+        cand = (int32_t)old;
+    }
     if (act && !later) {
-        if (BIG) {
+        if (U32) {
             table32[h] = (uint32_t)p;
         } else {
             table16[h] = (uint16_t)p;
@@ -337,7 +358,7 @@ __device__ __forceinline__ void chunk_issue(Chunk& C, const uint8_t* s, uint32_t
     C.v = v;
     C.cand = cand;
     // LZ4_DISTANCE_MAX (lz4.c:1064): only checkable past 64 KiB
-    C.okc = act && cand >= 0 && p <= mlast && (!BIG || p - cand <= 65535);
+    C.okc = act && cand >= 0 && p <= mlast && (!U32 || p - cand <= 65535);
     // every address stays inside the block (N >= 4 here; p <= mlast when okc)
     const int32_t cs = C.okc ? cand : 0;
     const int32_t ps = C.okc ? p : 0;
@@ -371,15 +392,15 @@ __device__ __forceinline__ uint64_t chunk_finish(const Chunk& C, int32_t p0, int
 #ifndef LZ4M_PC_ORDER
 #define LZ4M_PC_ORDER 1   // 1: B's candidate loads after A's walk (r05f: +0.7-1 %); 0: before
 #endif
-template <bool BIG, int HB>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BIG || HB > 12 ? 1 : 5))) void pcompress_kernel(const uint8_t* __restrict__ src,
+template <bool BIG, int HB, bool WIN = false>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((BIG && !WIN) || HB > 12 ? 1 : 5))) void pcompress_kernel(const uint8_t* __restrict__ src,
                                                        const int64_t* __restrict__ src_off,
                                                        const int32_t* __restrict__ src_len, uint8_t* __restrict__ dst,
                                                        const int64_t* __restrict__ dst_off,
                                                        const int32_t* __restrict__ dst_cap,
                                                        int32_t* __restrict__ out_len, int64_t n) {
     // 8192 hash4 entries: u16 positions (blocks <= 64 KiB) or u32 (BIG)
-    constexpr int kWords = BIG ? (1 << HB) : (1 << HB) / 2;   // table size in u32 words
+    constexpr int kWords = (BIG && !WIN) ? (1 << HB) : (1 << HB) / 2;   // table size in u32 words
     __shared__ __attribute__((aligned(16))) uint32_t table[kWords];
     const uint32_t lane = threadIdx.x;
     for (int64_t b = blockIdx.x; b < n; b += gridDim.x) {
@@ -403,7 +424,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BIG || HB > 
         uint64_t mask = 0;
         uint32_t wnext = 0;   // the hash word of the chunk after next, loaded a chunk ahead
         if (N >= 4) {
-            chunk_issue<BIG, HB>(A, s, table, 0, load_word(s, (int32_t)lane, N), N, mlast, lane);
+            chunk_issue<BIG, HB, WIN>(A, s, table, 0, load_word(s, (int32_t)lane, N), N, mlast, lane);
             mask = chunk_finish(A, 0, matchlimit, L, back, lane);
             if (68 <= N) wnext = load_word(s, 64 + (int32_t)lane, N);
         }
@@ -420,7 +441,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BIG || HB > 
             // loads in order: such a wait would also wait for B's)
             auto issue_b = [&]() __attribute__((always_inline)) {
                 if (has_next) {
-                    chunk_issue<BIG, HB>(B, s, table, p0 + 64, wnext, N, mlast, lane);
+                    chunk_issue<BIG, HB, WIN>(B, s, table, p0 + 64, wnext, N, mlast, lane);
                     if (p0 + 132 <= N) wafter = load_word(s, p0 + 128 + (int32_t)lane, N);
                 }
             };
@@ -536,14 +557,28 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BIG || HB > 
 }
 
 // variant: 0 = blocks <= 64 KiB, 12-bit u16 table; 1 = the same with 13 bits;
-// 2 = any block size, 13-bit u32 table
+// 2 = any block size: a 13-bit u32 table, or (LZ4M_PC_LARGE) a windowed u16 table
+#ifndef LZ4M_PC_LARGE_DEFAULT
+#define LZ4M_PC_LARGE_DEFAULT 13   // r05ay: 303 -> 167 ms on config 4, same size
+#endif
 int pcompress_launch(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len, uint8_t* d_dst,
                      const int64_t* d_dst_off, const int32_t* d_dst_cap, int32_t* d_out_len, int64_t n, int variant,
                      hipStream_t stream) {
     const uint32_t grid = (uint32_t)(n < (1ll << 30) ? n : (1ll << 30));
     if (variant == 2) {
-        hipLaunchKernelGGL((pcompress_kernel<true, 13>), dim3(grid), dim3(64), 0, stream, d_src, d_src_off, d_src_len,
-                           d_dst, d_dst_off, d_dst_cap, d_out_len, n);
+        static const int large = [] {   // LZ4M_PC_LARGE (A/B): 0 = u32 table, 12 / 13 = windowed u16 table of that many bits
+            const char* e = getenv("LZ4M_PC_LARGE");
+            return e ? atoi(e) : LZ4M_PC_LARGE_DEFAULT;
+        }();
+        if (large == 12)
+            hipLaunchKernelGGL((pcompress_kernel<true, 12, true>), dim3(grid), dim3(64), 0, stream, d_src, d_src_off,
+                               d_src_len, d_dst, d_dst_off, d_dst_cap, d_out_len, n);
+        else if (large == 13)
+            hipLaunchKernelGGL((pcompress_kernel<true, 13, true>), dim3(grid), dim3(64), 0, stream, d_src, d_src_off,
+                               d_src_len, d_dst, d_dst_off, d_dst_cap, d_out_len, n);
+        else
+            hipLaunchKernelGGL((pcompress_kernel<true, 13>), dim3(grid), dim3(64), 0, stream, d_src, d_src_off,
+                               d_src_len, d_dst, d_dst_off, d_dst_cap, d_out_len, n);
     } else if (variant == 1) {
         hipLaunchKernelGGL((pcompress_kernel<false, 13>), dim3(grid), dim3(64), 0, stream, d_src, d_src_off,
                            d_src_len, d_dst, d_dst_off, d_dst_cap, d_out_len, n);

@@ -303,6 +303,29 @@ def test_parallel_parse_ratio(gpu, oracle, kind, variant, tol):
         assert _decodes(oracle, g, b)
 
 
+@pytest.mark.parametrize("kind", ["text", "markup", "runs", "random", "silesia"])
+def test_parallel_parse_large_blocks(gpu, oracle, kind):
+    """PARSE_PARALLEL_LARGE (blocks > 64 KiB: frame blocks of 256 KiB - 4 MiB)
+    on 4 MiB, odd and just-over-64-KiB blocks, plus periodic data whose
+    repeats sit at offsets 65535 / 65536 / 65537 (the window edge: a match at
+    distance 65536 is not encodable, lz4.c:1064).  Every block decodes
+    exactly with the reference decoder and stays within 5 % of
+    LZ4_compress_default's size."""
+    raw = _synth.blocks(2 * 64 + 8, kind, seed=41).tobytes()
+    src = [raw[:4 << 20], raw[(4 << 20):(4 << 20) + 300_001], raw[-65537:]]
+    rng = np.random.default_rng(5)
+    for period in (65535, 65536, 65537):
+        unit = rng.integers(0, 256, period, dtype=np.uint8).tobytes()
+        src.append((unit * 4)[:3 * period + 1000])
+    got = gpu_compress(src, N.PARSE_PARALLEL_LARGE, gpu)
+    for i, b in enumerate(src):
+        assert got[i] is not None and len(got[i]) <= N.compress_bound(len(b)), i
+        assert _decodes(oracle, got[i], b), (i, len(b))
+    ours = sum(len(g) for g in got[:3])
+    ref = sum(len(oracle.compress(b)) for b in src[:3])
+    assert ours <= 1.05 * ref, (kind, ours, ref)
+
+
 def test_parallel_parse_limited_output(gpu, oracle, corpus):
     blocks, _ = corpus
     noise = np.random.default_rng(3).integers(0, 256, 65536, dtype=np.uint8).tobytes()
