@@ -4,7 +4,8 @@ launch ends (HIP events) and when the host hash gets to each 64 MiB piece,
 relative to the call's start.  Shows whether the hash waits for the decode
 (the decode launches must stay ahead of ~13.8 GB/s of hashing).
 FOLLOW_CHUNKS=<k> overrides the launch count, DECODER=<name> forces the
-decoder of the launches (lz4._native.DECODERS)."""
+decoder of the launches (lz4._native.DECODERS); LZ4M_FOLLOW_SPLIT=0 the
+round-5 layout of equal launches on one stream."""
 import os
 import sys
 import threading
@@ -54,7 +55,7 @@ def launch(*a, **k):
         k["decoder"] = DEC
     orig_launch(*a, **k)
     e = torch.cuda.Event(enable_timing=True)
-    e.record()
+    e.record(k.get("stream"))
     launch_evs.append((time.perf_counter(), e))
 
 
