@@ -128,6 +128,22 @@ int lz4m_compress_linked_batch(const uint8_t* d_src, const int64_t* d_src_off, c
                                const int32_t* d_dst_cap, int32_t* d_out_len, int64_t n, int acceleration,
                                int mode, void* d_work, size_t work_bytes, lz4m_stream_t stream);
 
+/*
+ * LZ4M_PARSE_PARALLEL_LARGE for batches of few large blocks (lz4.frame with
+ * 256 KiB - 4 MiB independent blocks and parse="parallel", no reference
+ * counterpart: the reference compresses such a frame's blocks one by one,
+ * lz4frame.c:865-871).  Each block is parsed as up to 16 segments of >= 256
+ * KiB, one wavefront each, then joined (valid LZ4 blocks, not the exact
+ * parse).  Blocks longer than max_len report 0 (not compressed).  Needs
+ * lz4m_pcompress_large_workspace_size(n, max_len) bytes of device scratch
+ * (about 16 x the largest block per block).  Stream-ordered, no sync.
+ */
+size_t lz4m_pcompress_large_workspace_size(int64_t n, int32_t max_len);
+int lz4m_pcompress_large_batch(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len,
+                               uint8_t* d_dst, const int64_t* d_dst_off, const int32_t* d_dst_cap,
+                               int32_t* d_out_len, int64_t n, int32_t max_len, void* d_work, size_t work_bytes,
+                               lz4m_stream_t stream);
+
 /* Library identification (mirrors LZ4_versionNumber, lz4.c:728, of the
  * format version this codec is bit-compatible with: 10904). */
 int lz4m_version_number(void);

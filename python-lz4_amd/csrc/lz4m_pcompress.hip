@@ -392,47 +392,99 @@ __device__ __forceinline__ uint64_t chunk_finish(const Chunk& C, int32_t p0, int
 #ifndef LZ4M_PC_ORDER
 #define LZ4M_PC_ORDER 1   // 1: B's candidate loads after A's walk (r05f: +0.7-1 %); 0: before
 #endif
-template <bool BIG, int HB, bool WIN = false>
+// SEG (blocks > 64 KiB, lz4m_pcompress_large_batch): a block is parsed as
+// up to kSegs segments of >= 256 KiB, one wavefront each, so that a batch of
+// few large blocks (config 4: 2 048 x 4 MiB) still fills the chip.  Segment k
+// parses [lo, hi) with a fresh table and its own anchor at lo: its matches
+// start at or before hi - 4 and end at or before hi (and within the block's
+// MFLIMIT / LASTLITERALS, lz4.c:942-943), and a segment other than the last writes no
+// last-literals sequence.  Its sequences go to a scratch slot with, in
+// seg_meta: bytes written, end anchor, the first sequence's literal length
+// (-1: none) and match length.  pcompress_stitch_kernel then joins the slots
+// into the block: the literals a segment leaves pending are merged into the
+// next first sequence's literal run (its token and length bytes rewritten),
+// which is the only place two segments' sequences meet.
+constexpr int kSegs = 16;
+constexpr int32_t kSegMin = 256 << 10;
+
+__host__ __device__ inline int32_t seg_len(int32_t n) {
+    const int32_t q = (int32_t)((((int64_t)n + kSegs - 1) / kSegs + 63) & ~(int64_t)63);
+    return q > kSegMin ? q : kSegMin;
+}
+// scratch bytes of one segment slot (>= LZ4_compressBound of the segment)
+__host__ __device__ inline int64_t seg_slot(int32_t seg) { return (((int64_t)seg + seg / 255 + 80) + 15) & ~(int64_t)15; }
+
+template <bool BIG, int HB, bool WIN = false, bool SEG = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((BIG && !WIN) || HB > 12 ? 1 : 5))) void pcompress_kernel(const uint8_t* __restrict__ src,
                                                        const int64_t* __restrict__ src_off,
                                                        const int32_t* __restrict__ src_len, uint8_t* __restrict__ dst,
                                                        const int64_t* __restrict__ dst_off,
                                                        const int32_t* __restrict__ dst_cap,
-                                                       int32_t* __restrict__ out_len, int64_t n) {
+                                                       int32_t* __restrict__ out_len, int64_t n,
+                                                       int32_t* __restrict__ seg_meta = nullptr, int64_t seg_cap = 0) {
+    static_assert(!SEG || (BIG && WIN), "segments are parsed with the windowed table");
     // 8192 hash4 entries: u16 positions (blocks <= 64 KiB) or u32 (BIG)
     constexpr int kWords = (BIG && !WIN) ? (1 << HB) : (1 << HB) / 2;   // table size in u32 words
     __shared__ __attribute__((aligned(16))) uint32_t table[kWords];
     const uint32_t lane = threadIdx.x;
-    for (int64_t b = blockIdx.x; b < n; b += gridDim.x) {
-        const int32_t N = src_len[b];
-        const int32_t cap = dst_cap[b];
-        const uint8_t* s = src + src_off[b];
-        uint8_t* d = dst + dst_off[b];
-        if (N < 0 || (!BIG && N > 65536)) {   // the u16 table covers blocks up to 64 KiB
-            if (lane == 0) out_len[b] = 0;
-            continue;
+    const int64_t items = SEG ? n * kSegs : n;
+    for (int64_t b = blockIdx.x; b < items; b += gridDim.x) {
+        int32_t N, cap, lo = 0, mlast, matchlimit;
+        bool fin = true;
+        const uint8_t* s;
+        uint8_t* d;
+        if (SEG) {
+            const int64_t blk = b / kSegs;
+            const int32_t k = (int32_t)(b % kSegs), NB = src_len[blk];
+            const int32_t seg = NB > 0 ? seg_len(NB) : kSegMin;
+            const int64_t lo64 = (int64_t)k * seg;
+            if (NB < 0 || seg_slot(seg) > seg_cap || (k > 0 && lo64 >= NB)) {   // no such segment / bad block
+                if (lane == 0)
+                    reinterpret_cast<int4*>(seg_meta)[b] = make_int4(NB < 0 || seg_slot(seg) > seg_cap ? -1 : 0, 0, -1, 0);
+                continue;
+            }
+            lo = (int32_t)lo64;
+            const int32_t hi = NB - lo > seg ? lo + seg : NB;
+            fin = hi == NB;
+            N = fin || NB - hi < 3 ? NB : hi + 3;   // positions < hi have their 4 hash bytes (inside the block)
+            // the block's MFLIMIT / LASTLITERALS bind every segment (a short last segment)
+            mlast = fin || hi - 4 > NB - 12 ? NB - 12 : hi - 4;
+            matchlimit = fin || hi > NB - 5 ? NB - 5 : hi;
+            s = src + src_off[blk];
+            d = dst + b * seg_cap;
+            cap = (int32_t)seg_cap;
+        } else {
+            N = src_len[b];
+            cap = dst_cap[b];
+            s = src + src_off[b];
+            d = dst + dst_off[b];
+            if (N < 0 || (!BIG && N > 65536)) {   // the u16 table covers blocks up to 64 KiB
+                if (lane == 0) out_len[b] = 0;
+                continue;
+            }
+            mlast = N - 12;      // last match start (MFLIMIT)
+            matchlimit = N - 5;  // match end bound (LASTLITERALS)
         }
         for (int k = (int)lane; k < kWords / 4; k += 64)
             reinterpret_cast<u32x4*>(table)[k] = u32x4{0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
-        int32_t anchor = 0, cur = 0, op = 0;
+        int32_t anchor = lo, cur = lo, op = 0;
+        int32_t f_lit = -1, f_ml = 0;   // SEG: the first sequence's literal and match lengths
         bool fail = false;
-        const int32_t mlast = N - 12;      // last match start (MFLIMIT)
-        const int32_t matchlimit = N - 5;  // match end bound (LASTLITERALS)
         uint32_t vprev = 0;
         Chunk A;
         int32_t L = 0, back = 0;
         uint64_t mask = 0;
         uint32_t wnext = 0;   // the hash word of the chunk after next, loaded a chunk ahead
-        if (N >= 4) {
-            chunk_issue<BIG, HB, WIN>(A, s, table, 0, load_word(s, (int32_t)lane, N), N, mlast, lane);
-            mask = chunk_finish(A, 0, matchlimit, L, back, lane);
-            if (68 <= N) wnext = load_word(s, 64 + (int32_t)lane, N);
+        if (N - lo >= 4) {
+            chunk_issue<BIG, HB, WIN>(A, s, table, lo, load_word(s, lo + (int32_t)lane, N), N, mlast, lane);
+            mask = chunk_finish(A, lo, matchlimit, L, back, lane);
+            if (lo + 68 <= N) wnext = load_word(s, lo + 64 + (int32_t)lane, N);
         }
         // Per chunk: issue B's loads (and the word of the chunk after B),
         // walk A, finish B, then encode A.  No store sits between a load and
         // its use, so every wait is for loads only (gfx9 counts stores in
         // vmcnt, and a wait behind a variable number of stores is vmcnt(0)).
-        for (int32_t p0 = 0; p0 + 4 <= N; p0 += 64) {
+        for (int32_t p0 = lo; p0 + 4 <= N; p0 += 64) {
             const bool has_next = p0 + 68 <= N;
             Chunk B;
             uint32_t wafter = 0;
@@ -523,6 +575,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((BIG && !WIN
             uint64_t maskB = 0;
             if (!LZ4M_PC_ORDER && has_next) maskB = chunk_finish(B, p0 + 64, matchlimit, LB, backB, lane);
             if (ns > 0) {
+                if (SEG && f_lit < 0) {
+                    f_lit = rdl(q_lit, 0);
+                    f_ml = rdl(q_ml, 0);
+                }
                 const int32_t w = emit_seqs<BIG>(s, d, op, cap, ns, q_ls, q_lit, q_off, q_ml, q_ob, q_pb, acc, pacc, p0,
                                             A.v, vprev, lane);
                 if (w < 0) {
@@ -541,8 +597,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((BIG && !WIN
             back = backB;
             wnext = wafter;
         }
-        if (!fail) {   // last literals (lz4.c:1266-1293)
+        if (!fail && fin) {   // last literals (lz4.c:1266-1293)
             const int32_t lit = N - anchor;
+            if (SEG && f_lit < 0) f_lit = lit;
             const int32_t sz = seq_size<BIG>(lit, 0);
             const int32_t w = emit_seqs<BIG>(s, d, op, cap, 1, anchor, lit, 0, 0, 0, 0, sz,
                                         lit >= kLongLit ? sz - lit : sz, 1 << 30, 0u, 0u, lane);
@@ -552,8 +609,136 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((BIG && !WIN
                 op += w;
             }
         }
-        if (lane == 0) out_len[b] = fail ? 0 : op;
+        if (lane == 0) {
+            if (SEG)
+                reinterpret_cast<int4*>(seg_meta)[b] = make_int4(fail ? -1 : op, anchor, f_lit, f_ml);
+            else
+                out_len[b] = fail ? 0 : op;
+        }
     }
+}
+
+// len bytes from s to d by the wave, 16 per lane, four loads in flight
+__device__ __forceinline__ void wave_copy(uint8_t* __restrict__ d, const uint8_t* __restrict__ s, int32_t len,
+                                          uint32_t lane) {
+    int32_t x = 16 * (int32_t)lane;
+    for (; x + 3 * 1024 + 16 <= len; x += 4 * 1024) {
+        const u32x4 a = ld16(s + x), b = ld16(s + x + 1024), c = ld16(s + x + 2048), e = ld16(s + x + 3072);
+        st16(d + x, a);
+        st16(d + x + 1024, b);
+        st16(d + x + 2048, c);
+        st16(d + x + 3072, e);
+    }
+    for (; x < len; x += 1024) {
+        if (x + 16 <= len) {
+            st16(d + x, ld16(s + x));
+        } else {
+            for (int32_t y = x; y < len; ++y) d[y] = s[y];
+        }
+    }
+}
+
+// Joins a block's segment slots (SEG above): segment k's first sequence
+// takes the literals from the previous segments' end anchor c_k (the last
+// segment with a sequence before it; 0 for the first), so its token and
+// length bytes are rewritten and those literals copied from the source; the
+// rest of the slot is copied as it is.  The block fails (0) if a segment
+// failed or the joined size exceeds dst_cap.
+__global__ __launch_bounds__(64) void pcompress_stitch_kernel(const uint8_t* __restrict__ src,
+                                                              const int64_t* __restrict__ src_off,
+                                                              const int32_t* __restrict__ src_len,
+                                                              uint8_t* __restrict__ dst,
+                                                              const int64_t* __restrict__ dst_off,
+                                                              const int32_t* __restrict__ dst_cap,
+                                                              int32_t* __restrict__ out_len, int64_t n,
+                                                              const uint8_t* __restrict__ slots,
+                                                              const int32_t* __restrict__ seg_meta, int64_t seg_cap) {
+    const uint32_t lane = threadIdx.x;
+    for (int64_t b = blockIdx.x; b < n; b += gridDim.x) {
+        const int32_t NB = src_len[b];
+        if (NB < 0) {
+            if (lane == 0) out_len[b] = 0;
+            continue;
+        }
+        const int32_t seg = NB > 0 ? seg_len(NB) : kSegMin;
+        const int nseg = NB > 0 ? (int)(((int64_t)NB + seg - 1) / seg) : 1;
+        int4 m = make_int4(0, 0, -1, 0);
+        if ((int)lane < nseg) m = reinterpret_cast<const int4*>(seg_meta)[b * kSegs + lane];
+        const bool bad = __ballot((int)lane < nseg && m.x < 0) != 0;
+        // c_k: the end anchor of the last segment before k with a sequence
+        int32_t c = 0, my_c = 0;
+        for (int k = 0; k < nseg; ++k) {
+            if ((int)lane == k) my_c = c;
+            if (rdl(m.z, k) >= 0) c = rdl(m.y, k);
+        }
+        int32_t L1 = 0, nk = 0;
+        const bool has = (int)lane < nseg && m.z >= 0;
+        if (has) {
+            L1 = (int32_t)lane * seg + m.z - my_c;   // merged literal run of the first sequence
+            nk = 1 + ext_len<true>(L1) + L1 + (m.x - 1 - ext_len<true>(m.z) - m.z);
+        }
+        const int32_t incl = wave_incl_sum(nk), total = rdl(incl, 63);
+        if (bad || total > dst_cap[b]) {
+            if (lane == 0) out_len[b] = 0;
+            continue;
+        }
+        const uint8_t* s = src + src_off[b];
+        uint8_t* d = dst + dst_off[b];
+        for (int k = 0; k < nseg; ++k) {
+            if (rdl(m.z, k) < 0) continue;
+            const int32_t F = rdl(incl - nk, k), L = rdl(L1, k), ck = rdl(my_c, k), ml = rdl(m.w, k);
+            const int32_t l0 = rdl(m.z, k), o = rdl(m.x, k);
+            const int32_t E = ext_len<true>(L);
+            const uint32_t tok = (uint32_t)(((L < 15 ? L : 15) << 4) | (ml ? (ml - 4 < 15 ? ml - 4 : 15) : 0));
+            uint8_t* q = d + F;
+            for (int32_t x = (int32_t)lane; x <= E; x += 64)
+                q[x] = (uint8_t)(x == 0 ? tok : x < E ? 255u : (uint32_t)(L - 15 - 255 * (E - 1)));
+            wave_copy(q + 1 + E, s + ck, L, lane);
+            const int32_t h0 = 1 + ext_len<true>(l0) + l0;   // the slot's own first token, length bytes, literals
+            wave_copy(q + 1 + E + L, slots + (b * kSegs + k) * seg_cap + h0, o - h0, lane);
+        }
+        if (lane == 0) out_len[b] = total;
+    }
+}
+
+extern "C" size_t lz4m_pcompress_large_workspace_size(int64_t n, int32_t max_len) {
+    if (n <= 0 || max_len < 0) return 0;
+    const int64_t meta = (n * kSegs * 16 + 255) & ~(int64_t)255;
+    return (size_t)(meta + n * kSegs * seg_slot(max_len > 0 ? seg_len(max_len) : kSegMin));
+}
+
+#ifndef LZ4M_PC_SEGHB
+#define LZ4M_PC_SEGHB 12   // hash bits of the segment parse
+#endif
+extern "C" int lz4m_pcompress_large_batch(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len,
+                                          uint8_t* d_dst, const int64_t* d_dst_off, const int32_t* d_dst_cap,
+                                          int32_t* d_out_len, int64_t n, int32_t max_len, void* d_work,
+                                          size_t work_bytes, lz4m_stream_t stream) {
+    if (n < 0 || max_len < 0) return LZ4M_EINVAL;
+    if (n == 0) return 0;
+    if (d_work == nullptr || work_bytes < lz4m_pcompress_large_workspace_size(n, max_len)) return LZ4M_EINVAL;
+    hipStream_t st = (hipStream_t)stream;
+    int32_t* meta = (int32_t*)d_work;
+    uint8_t* slots = (uint8_t*)d_work + ((n * kSegs * 16 + 255) & ~(int64_t)255);
+    const int64_t cap = seg_slot(max_len > 0 ? seg_len(max_len) : kSegMin);
+    static const int hb = [] {
+        const char* e = getenv("LZ4M_PC_SEGHB");   // A/B: 12 or 13
+        return e ? atoi(e) : LZ4M_PC_SEGHB;
+    }();
+    const int64_t items = n * kSegs;
+    const uint32_t grid = (uint32_t)(items < (1ll << 30) ? items : (1ll << 30));
+    if (hb == 13)
+        hipLaunchKernelGGL((pcompress_kernel<true, 13, true, true>), dim3(grid), dim3(64), 0, st, d_src, d_src_off,
+                           d_src_len, slots, nullptr, nullptr, nullptr, n, meta, cap);
+    else
+        hipLaunchKernelGGL((pcompress_kernel<true, 12, true, true>), dim3(grid), dim3(64), 0, st, d_src, d_src_off,
+                           d_src_len, slots, nullptr, nullptr, nullptr, n, meta, cap);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+    const uint32_t sgrid = (uint32_t)(n < (1ll << 30) ? n : (1ll << 30));
+    hipLaunchKernelGGL(pcompress_stitch_kernel, dim3(sgrid), dim3(64), 0, st, d_src, d_src_off, d_src_len, d_dst,
+                       d_dst_off, d_dst_cap, d_out_len, n, slots, meta, cap);
+    return (int)hipGetLastError();
 }
 
 // variant: 0 = blocks <= 64 KiB, 12-bit u16 table; 1 = the same with 13 bits;

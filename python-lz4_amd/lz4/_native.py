@@ -58,6 +58,8 @@ def _declare(lib) -> None:
         "lz4m_compress_prefix_batch": ([vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, vp], i32),
         "lz4m_compress_linked_workspace_size": ([i64], C.c_size_t),
         "lz4m_compress_linked_passes": ([], i32),
+        "lz4m_pcompress_large_workspace_size": ([i64, i32], C.c_size_t),
+        "lz4m_pcompress_large_batch": ([vp, vp, vp, vp, vp, vp, vp, i64, i32, vp, C.c_size_t, vp], i32),
         "lz4m_compress_linked_batch": ([vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, vp, C.c_size_t, vp], i32),
         "lz4m_xxh32_batch": ([vp, vp, vp, u32, vp, i64, vp], i32),
         "lz4m_xxh32_long": ([vp, i64, u32, vp, vp], i32),
@@ -212,9 +214,24 @@ def launch_decompress_chain(src, src_off, src_len, raw_mask, dst, status, n, max
     check(rc, "lz4m_decompress_chain")
 
 
-def launch_compress(src, src_off, src_len, dst, dst_off, dst_cap, out_len, n, table, accel, stream=None) -> None:
-    rc = lib().lz4m_compress_batch(ptr(src), ptr(src_off), ptr(src_len), ptr(dst), ptr(dst_off), ptr(dst_cap),
-                                   ptr(out_len), n, table, accel, stream_ptr(stream))
+def launch_compress(src, src_off, src_len, dst, dst_off, dst_cap, out_len, n, table, accel, stream=None,
+                    max_len: int | None = None) -> None:
+    """Batched compression (lz4m_compress_batch).  PARSE_PARALLEL_LARGE with
+    ``max_len`` (the longest block) parses each block as up to 16 segments
+    (lz4m_pcompress_large_batch; LZ4M_PC_SEG=0: one wavefront per block)."""
+    L = lib()
+    if table == PARSE_PARALLEL_LARGE and max_len is not None and os.environ.get("LZ4M_PC_SEG", "1") != "0":
+        s = stream if stream is not None else torch.cuda.current_stream(src.device)
+        with torch.cuda.stream(s):   # (allocated on the stream that uses it)
+            work = torch.empty(int(L.lz4m_pcompress_large_workspace_size(n, max_len)), dtype=torch.uint8,
+                               device=src.device)
+        rc = L.lz4m_pcompress_large_batch(ptr(src), ptr(src_off), ptr(src_len), ptr(dst), ptr(dst_off),
+                                          ptr(dst_cap), ptr(out_len), n, max_len, ptr(work), work.numel(),
+                                          stream_ptr(stream))
+        check(rc, "lz4m_pcompress_large_batch")
+        return
+    rc = L.lz4m_compress_batch(ptr(src), ptr(src_off), ptr(src_len), ptr(dst), ptr(dst_off), ptr(dst_cap),
+                               ptr(out_len), n, table, accel, stream_ptr(stream))
     check(rc, "lz4m_compress_batch")
 
 

@@ -296,7 +296,8 @@ def _compress_frame(d_src, n=None, *, compression_level=0, block_size=0, content
                 table = N.TABLE_AUTO
             else:
                 table = N.PARSE_PARALLEL if bsize <= 65536 else N.PARSE_PARALLEL_LARGE
-            N.launch_compress(d_src, raw_off, raw_len, cmp, cmp_off, cap, cmp_len, nb, table, accel, stream)
+            N.launch_compress(d_src, raw_off, raw_len, cmp, cmp_off, cap, cmp_len, nb, table, accel, stream,
+                              max_len=bsize)
         rec_len = torch.empty(nb, dtype=torch.int32, device=dev)
         N.frame_block_sizes(raw_len, cmp_len, block_checksum, rec_len, nb, stream)
         frame_off = N.exclusive_scan(rec_len, stream=stream)

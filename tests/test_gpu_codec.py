@@ -50,7 +50,7 @@ def gpu_decompress(blocks, caps, dev, decoder="auto"):
     return out
 
 
-def gpu_compress(blocks, table, dev, accel=1, caps=None):
+def gpu_compress(blocks, table, dev, accel=1, caps=None, max_len=None):
     packed, offs, lens = _pack(blocks)
     caps = caps or [N.compress_bound(L) for L in lens]
     d_src = N.to_device(packed, dev)
@@ -63,7 +63,8 @@ def gpu_compress(blocks, table, dev, accel=1, caps=None):
     N.launch_compress(d_src, torch.tensor(offs, dtype=torch.int64, device=dev),
                       torch.tensor(lens, dtype=torch.int32, device=dev), d_dst,
                       torch.tensor(d_off, dtype=torch.int64, device=dev),
-                      torch.tensor(caps, dtype=torch.int32, device=dev), ol, len(blocks), table, accel)
+                      torch.tensor(caps, dtype=torch.int32, device=dev), ol, len(blocks), table, accel,
+                      max_len=max_len)
     host = d_dst.cpu().numpy()
     return [host[d_off[i]:d_off[i] + L].tobytes() if L > 0 else None for i, L in enumerate(ol.cpu().tolist())]
 
@@ -303,27 +304,59 @@ def test_parallel_parse_ratio(gpu, oracle, kind, variant, tol):
         assert _decodes(oracle, g, b)
 
 
+@pytest.mark.parametrize("seg", [True, False])
 @pytest.mark.parametrize("kind", ["text", "markup", "runs", "random", "silesia"])
-def test_parallel_parse_large_blocks(gpu, oracle, kind):
+def test_parallel_parse_large_blocks(gpu, oracle, kind, seg):
     """PARSE_PARALLEL_LARGE (blocks > 64 KiB: frame blocks of 256 KiB - 4 MiB)
     on 4 MiB, odd and just-over-64-KiB blocks, plus periodic data whose
     repeats sit at offsets 65535 / 65536 / 65537 (the window edge: a match at
     distance 65536 is not encodable, lz4.c:1064).  Every block decodes
     exactly with the reference decoder and stays within 5 % of
-    LZ4_compress_default's size."""
+    LZ4_compress_default's size.  seg: the segmented parse
+    (lz4m_pcompress_large_batch, what lz4.frame uses) or one wavefront per
+    block."""
     raw = _synth.blocks(2 * 64 + 8, kind, seed=41).tobytes()
     src = [raw[:4 << 20], raw[(4 << 20):(4 << 20) + 300_001], raw[-65537:]]
     rng = np.random.default_rng(5)
     for period in (65535, 65536, 65537):
         unit = rng.integers(0, 256, period, dtype=np.uint8).tobytes()
         src.append((unit * 4)[:3 * period + 1000])
-    got = gpu_compress(src, N.PARSE_PARALLEL_LARGE, gpu)
+    got = gpu_compress(src, N.PARSE_PARALLEL_LARGE, gpu, max_len=max(map(len, src)) if seg else None)
     for i, b in enumerate(src):
         assert got[i] is not None and len(got[i]) <= N.compress_bound(len(b)), i
         assert _decodes(oracle, got[i], b), (i, len(b))
     ours = sum(len(g) for g in got[:3])
     ref = sum(len(oracle.compress(b)) for b in src[:3])
     assert ours <= 1.05 * ref, (kind, ours, ref)
+
+
+def test_parallel_parse_segment_joins(gpu, oracle):
+    """The segmented large-block parse (lz4m_pcompress_large_batch): segment
+    edges at every size class -- one segment, a last segment of 1, 2, 3 and
+    13 bytes, segments longer than 256 KiB (blocks over 4 MiB), empty blocks
+    -- and literals carried across segments without a match (incompressible
+    segments before compressible ones: the first sequence after them takes
+    a literal run of ~700 KiB).  Every block decodes exactly with the
+    reference decoder; a block whose joined size exceeds its capacity
+    reports 0 (None)."""
+    rng = np.random.default_rng(9)
+    text = _synth.blocks(160, "text", seed=3).tobytes()
+    seg = 256 << 10
+    src = [b"", b"abcd" * 3, text[:seg], text[:seg + 1], text[:seg + 2], text[:seg + 3], text[:2 * seg + 13],
+           text[:(4 << 20) + 4097], text[:5 * seg + 17],
+           rng.integers(0, 256, 700 << 10, dtype=np.uint8).tobytes() + text[:500 << 10],
+           rng.integers(0, 256, seg, dtype=np.uint8).tobytes() + b"z" * 5 + rng.integers(0, 256, seg, dtype=np.uint8).tobytes(),
+           text[:seg] + rng.integers(0, 256, 3 * seg, dtype=np.uint8).tobytes()]
+    got = gpu_compress(src, N.PARSE_PARALLEL_LARGE, gpu, max_len=max(map(len, src)))
+    for i, b in enumerate(src):
+        assert got[i] is not None and len(got[i]) <= N.compress_bound(len(b)), i
+        assert _decodes(oracle, got[i], b), (i, len(b))
+    # limited output: an incompressible block does not fit size - 1; a compressible one does
+    noise = rng.integers(0, 256, 3 * seg, dtype=np.uint8).tobytes()
+    lim = [noise, text[:3 * seg]]
+    got = gpu_compress(lim, N.PARSE_PARALLEL_LARGE, gpu, caps=[len(b) - 1 for b in lim], max_len=3 * seg)
+    assert got[0] is None
+    assert got[1] is not None and _decodes(oracle, got[1], lim[1])
 
 
 def test_parallel_parse_limited_output(gpu, oracle, corpus):

@@ -1,6 +1,6 @@
 """Dev probe: config 4's device frame compress without a content checksum
 (8 GiB, 4 MiB independent blocks, parallel parse): the whole call against
-its compression launch alone, and the compressed size (LZ4M_PC_LARGE A/B)."""
+its compression launch alone, and the compressed size (LZ4M_PC_LARGE / LZ4M_PC_SEG / LZ4M_PC_SEGHB A/B)."""
 import os
 import sys
 import time
@@ -36,9 +36,11 @@ cmp_len = torch.empty(nb, dtype=torch.int32, device=dev)
 for rep in range(2):
     torch.cuda.synchronize()
     t = time.perf_counter()
-    N.launch_compress(src, raw_off, raw_len, cmp, cmp_off, raw_len - 1, cmp_len, nb, N.PARSE_PARALLEL_LARGE, 1)
+    N.launch_compress(src, raw_off, raw_len, cmp, cmp_off, raw_len - 1, cmp_len, nb, N.PARSE_PARALLEL_LARGE, 1,
+                      max_len=FB)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t
     print(f"compression launch alone: {dt * 1e3:.1f} ms", flush=True)
 tot = int(cmp_len.to(torch.int64).sum())
-print(f"LZ4M_PC_LARGE={os.environ.get('LZ4M_PC_LARGE', 'default')}: {tot} bytes, ratio {L / tot:.4f}", flush=True)
+tag = " ".join(f"{k}={os.environ[k]}" for k in ("LZ4M_PC_LARGE", "LZ4M_PC_SEG", "LZ4M_PC_SEGHB") if k in os.environ)
+print(f"[{tag or 'default'}] {tot} bytes, ratio {L / tot:.4f}", flush=True)
