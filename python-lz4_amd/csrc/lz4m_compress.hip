@@ -135,6 +135,46 @@ struct Table<LZ4M_TABLE_U32_HASH5> {   // 4096 x u32 (lz4.c:764-774, 834-838)
     }
 };
 
+// The byU32 / hash5 table (same hash, same semantics) for indexes below 2^17
+// -- the speculative linked passes, where an index is a byte of 64 KiB of
+// history + a block of <= 64 KiB: the low 16 bits of entry h are a u16 at
+// t[h] and bit 16 is bit h of a 4096-bit map behind them (8.5 KiB instead
+// of 16: 16 workgroups per CU instead of 9).  A store writes both parts; an
+// exchange swaps both, each with a masked OR on its enclosing dword (lanes on
+// one dword are applied in lane order, as Table<U32>::xchg's exchange).
+constexpr int kTableU17 = 0x117;
+constexpr int kU17Halves = 4096 + 256;   // table size in u16
+template <>
+struct Table<kTableU17> {
+    static constexpr int kEntries = 4096;
+    __device__ static __forceinline__ uint32_t hash(const uint8_t* p) { return Table<LZ4M_TABLE_U32_HASH5>::hash(p); }
+    __device__ static __forceinline__ uint32_t hash_v(u32x4 v) { return Table<LZ4M_TABLE_U32_HASH5>::hash_v(v); }
+    __device__ static __forceinline__ uint32_t get_v(uint16_t* t, uint32_t h) {
+        const uint32_t lo = ((volatile lds_t16*)t)[h];
+        const uint32_t m = ((volatile lds_t32*)(t + 4096))[h >> 5];
+        return lo | (((m >> (h & 31u)) & 1u) << 16);
+    }
+    __device__ static __forceinline__ uint32_t get(const uint16_t* t, uint32_t h) { return get_v((uint16_t*)t, h); }
+    __device__ static __forceinline__ void put_v(uint16_t* t, uint32_t h, uint32_t v) {
+        ((volatile lds_t16*)t)[h] = (uint16_t)v;
+        const uint32_t a = (uint32_t)(uintptr_t)((lds_t32*)(t + 4096) + (h >> 5)), b = 1u << (h & 31u);
+        asm volatile("ds_mskor_b32 %0, %1, %2" : : "v"(a), "v"(b), "v"(((v >> 16) & 1u) << (h & 31u)) : "memory");
+    }
+    __device__ static __forceinline__ void put(uint16_t* t, uint32_t h, uint32_t v) { put_v(t, h, v); }
+    static constexpr bool kDistCheck = true;
+    __device__ static __forceinline__ uint32_t xchg(uint16_t* t, uint32_t h, uint32_t v) {
+        const uint32_t a = (uint32_t)(uintptr_t)((lds_t16*)t + h) & ~3u, sh = (h & 1u) * 16u;
+        const uint32_t am = (uint32_t)(uintptr_t)((lds_t32*)(t + 4096) + (h >> 5)), bit = h & 31u;
+        uint32_t lo, hi;
+        asm volatile("ds_mskor_rtn_b32 %0, %2, %3, %4\n\tds_mskor_rtn_b32 %1, %5, %6, %7\n\ts_waitcnt lgkmcnt(0)"
+                     : "=&v"(lo), "=&v"(hi)
+                     : "v"(a), "v"(0xFFFFu << sh), "v"((v & 0xFFFFu) << sh), "v"(am), "v"(1u << bit),
+                       "v"(((v >> 16) & 1u) << bit)
+                     : "memory");
+        return ((lo >> sh) & 0xFFFFu) | (((hi >> bit) & 1u) << 16);
+    }
+};
+
 // LZ4M_CMP_XCHG: the search step inserts its 64 positions with one LDS
 // exchange per lane; lanes of a wave that hit the same bucket are applied in
 // lane order (gfx950: every one of 33.5 M instructions of random collision
@@ -1152,13 +1192,49 @@ __global__ __launch_bounds__(64) void compress_chain_kernel(const uint8_t* __res
 // When a pass changes no table, every block's last run used the table its
 // predecessor really leaves, and by induction from the stream's first block
 // (a fresh table) every output equals the serial chain's.
+// Entries 4k .. 4k+3 of a table in LDS as u32 (V = kTableU17: from the
+// split form; lanes 8j .. 8j+7 read one dword of the bit map)
+template <int V>
+__device__ __forceinline__ u32x4 tab_get4(const uint16_t* tab, int k) {
+    if constexpr (V == kTableU17) {
+        const uint64_t lo = *(const lds_vu64*)((const lds_u8*)tab + 8 * k);
+        const uint32_t m = *(const lds_t32*)(tab + 4096 + 2 * (k >> 3)) >> ((k & 7) * 4);
+        return u32x4{(uint32_t)(lo & 0xFFFFu) | ((m & 1u) << 16), (uint32_t)((lo >> 16) & 0xFFFFu) | ((m & 2u) << 15),
+                     (uint32_t)((lo >> 32) & 0xFFFFu) | ((m & 4u) << 14), (uint32_t)(lo >> 48) | ((m & 8u) << 13)};
+    } else {
+        return reinterpret_cast<const u32x4*>(tab)[k];
+    }
+}
+
+// Store entries 4k .. 4k+3 (values < 2^17 for kTableU17); the whole wave
+// calls it with k = lane + 64 i
+template <int V>
+__device__ __forceinline__ void tab_set4(uint16_t* tab, int k, u32x4 v, uint32_t lane) {
+    if constexpr (V == kTableU17) {
+        *(lds_vu64*)((lds_u8*)tab + 8 * k) = (uint64_t)((v.x & 0xFFFFu) | (v.y << 16)) |
+                                             ((uint64_t)((v.z & 0xFFFFu) | (v.w << 16)) << 32);
+        uint32_t m = (((v.x >> 16) & 1u) | ((v.y >> 15) & 2u) | ((v.z >> 14) & 4u) | ((v.w >> 13) & 8u))
+                     << ((k & 7) * 4);
+        m |= (uint32_t)__shfl_xor((int)m, 1);
+        m |= (uint32_t)__shfl_xor((int)m, 2);
+        m |= (uint32_t)__shfl_xor((int)m, 4);
+        if ((lane & 7u) == 0) *(lds_t32*)(tab + 4096 + 2 * (k >> 3)) = m;
+    } else {
+        reinterpret_cast<u32x4*>(tab)[k] = v;
+    }
+}
+
+// V: LZ4M_TABLE_U32_HASH5, or kTableU17 when every block is <= 64 KiB (a
+// larger one sets bit 2 of counters[1] and the host runs the U32 kernel)
+template <int V>
 __global__ __launch_bounds__(64) void compress_spec_kernel(
     const uint8_t* __restrict__ src, const int64_t* __restrict__ src_off, const int32_t* __restrict__ src_len,
     const int32_t* __restrict__ link, uint8_t* dst, const int64_t* __restrict__ dst_off,
     const int32_t* __restrict__ dst_cap, int32_t* __restrict__ out_len, int64_t n, int accel,
     const uint32_t* __restrict__ t_prev, uint32_t* __restrict__ t_cur, const uint8_t* __restrict__ chg_prev,
     uint8_t* __restrict__ chg_cur, int32_t* counters, int pass) {
-    __shared__ __attribute__((aligned(16))) uint16_t tab[8192];
+    constexpr bool U17 = V == kTableU17;
+    __shared__ __attribute__((aligned(16))) uint16_t tab[U17 ? kU17Halves : 8192];
     RING_DECL
     u32x4* t4 = reinterpret_cast<u32x4*>(tab);
     const uint32_t lane = threadIdx.x;
@@ -1187,16 +1263,25 @@ __global__ __launch_bounds__(64) void compress_spec_kernel(
             }
             hist = kWin;
         }
+        if (U17 && hist + len > 2 * (int64_t)kWin) {   // indexes past 2^17: the U32 kernel's job
+            if (lane == 0) atomicOr(&counters[1], 2);
+            continue;
+        }
         if (pass == 0 || !linked) {
-            zero_table(tab, lane);
+            if (U17) {
+                for (int k = lane; k < kU17Halves / 8; k += kWave) t4[k] = u32x4{0, 0, 0, 0};
+                __builtin_amdgcn_s_waitcnt(0xc07f);
+            } else {
+                zero_table(tab, lane);
+            }
         } else {
             const u32x4* pred = reinterpret_cast<const u32x4*>(t_prev + (size_t)(b - 1) * 4096);
-            for (int k = lane; k < 1024; k += kWave) t4[k] = pred[k];
+            for (int k = lane; k < 1024; k += kWave) tab_set4<V>(tab, k, pred[k], lane);
             __builtin_amdgcn_s_waitcnt(0xc07f);
         }
         const uint8_t* w = src + src_off[b] - hist;
-        const int64_t r = compress_block_w<LZ4M_TABLE_U32_HASH5>(w, hist, len, dst + dst_off[b], dst_cap[b],
-                                                                 accel, tab, ring, lane, 0u, 0u, 0, 0);
+        const int64_t r = compress_block_w<V>(w, hist, len, dst + dst_off[b], dst_cap[b],
+                                              accel, tab, ring, lane, 0u, 0u, 0, 0);
         if (lane == 0) out_len[b] = (int32_t)r;
         if (!feeds) {
             if (lane == 0) chg_cur[b] = 0;
@@ -1208,7 +1293,7 @@ __global__ __launch_bounds__(64) void compress_spec_kernel(
         bool diff = false;
         __builtin_amdgcn_s_waitcnt(0xc07f);
         for (int k = lane; k < 1024; k += kWave) {
-            u32x4 v = t4[k];
+            u32x4 v = tab_get4<V>(tab, k);
             v.x = v.x > shift ? v.x - shift : 0u;
             v.y = v.y > shift ? v.y - shift : 0u;
             v.z = v.z > shift ? v.z - shift : 0u;
@@ -1665,6 +1750,20 @@ extern "C" int lz4m_compress_linked_batch(const uint8_t* d_src, const int64_t* d
     g_linked_passes = 0;
     const int64_t lds_max = spec_lds_max();
     const bool verbose = getenv("LZ4M_SPEC_VERBOSE") != nullptr;
+    // LZ4M_SPEC_U17=0 (A/B): the batched passes keep the 16 KiB u32 table
+    bool u17 = [] {
+        const char* e = getenv("LZ4M_SPEC_U17");
+        return e == nullptr || atoi(e) != 0;
+    }();
+    // blocks the u32 kernel runs at once (9 workgroups per CU x the CUs)
+    static const int64_t u32_fit = [] {
+        int dev = 0, cus = 0, per = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &per, reinterpret_cast<const void*>(compress_spec_kernel<LZ4M_TABLE_U32_HASH5>), 64, 0);
+        return (int64_t)cus * per;
+    }();
     auto t_prev = std::chrono::steady_clock::now();
     for (int64_t pass = 0; pass <= n; ++pass) {
         g_linked_passes = (int)pass + 1;
@@ -1681,16 +1780,29 @@ extern "C" int lz4m_compress_linked_batch(const uint8_t* d_src, const int64_t* d
                                    d_src_len, d_link, d_dst, d_dst_off, d_dst_cap, d_out_len, n, acceleration,
                                    tb[prev], tb[cur], cb[cur], counters, list);
         } else {
-            hipLaunchKernelGGL(compress_spec_kernel, dim3(grid), dim3(64), 0, s, d_src, d_src_off, d_src_len, d_link,
-                               d_dst, d_dst_off, d_dst_cap, d_out_len, n, acceleration, tb[prev], tb[cur], cb[prev],
-                               cb[cur], counters, (int)pass);
+            // the split table pays when the u32 kernel's workgroups do not all fit at once
+            // (r05bd: 4 096 blocks 24.2 -> 18.7 ms; 1 180 blocks 14.5 -> 16.6 ms, so not there)
+            if (u17 && (pass == 0 || redo > u32_fit))
+                hipLaunchKernelGGL(compress_spec_kernel<kTableU17>, dim3(grid), dim3(64), 0, s, d_src, d_src_off,
+                                   d_src_len, d_link, d_dst, d_dst_off, d_dst_cap, d_out_len, n, acceleration, tb[prev],
+                                   tb[cur], cb[prev], cb[cur], counters, (int)pass);
+            else
+                hipLaunchKernelGGL(compress_spec_kernel<LZ4M_TABLE_U32_HASH5>, dim3(grid), dim3(64), 0, s, d_src,
+                                   d_src_off, d_src_len, d_link, d_dst, d_dst_off, d_dst_cap, d_out_len, n,
+                                   acceleration, tb[prev], tb[cur], cb[prev], cb[cur], counters, (int)pass);
         }
         e = hipGetLastError();
         if (e != hipSuccess) return (int)e;
         e = hipMemcpyAsync(h_counters, counters, 12, hipMemcpyDeviceToHost, s);
         if (e == hipSuccess) e = hipStreamSynchronize(s);
         if (e != hipSuccess) return (int)e;
-        if (h_counters[1]) return LZ4M_EINVAL;
+        if (h_counters[1] & 1) return LZ4M_EINVAL;
+        if (h_counters[1] & 2) {   // a block over 64 KiB: start again with the U32 table
+            u17 = false;
+            pass = -1;
+            h_counters[0] = 0;
+            continue;
+        }
         if (verbose) {   // (the host waits for every pass: its wall time is the pass's)
             const auto t_now = std::chrono::steady_clock::now();
             fprintf(stderr, "[lz4m] linked pass %d: %lld redone%s, %d tables changed, %.2f ms\n", (int)pass,

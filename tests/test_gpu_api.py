@@ -281,17 +281,20 @@ def _linked_case(gpu, data: bytes, bsize: int, accel: int, mode: int):
     return [h[k * slot: k * slot + ol[k]].tobytes() if ol[k] > 0 else None for k in range(nb)]
 
 
-@pytest.mark.parametrize("mode", ["serial", "speculative", "speculative-batched"])
+@pytest.mark.parametrize("mode", ["serial", "speculative", "speculative-batched", "speculative-batched-u32"])
 def test_linked_blocks_vs_oracle(gpu, oracle, mode, monkeypatch):
     """Linked streams of every kind and block size, both modes, against
     orc_compress_linked (pinned to the reference's linked frames).
     "speculative" runs every pass >= 1 of these small streams with the
     LDS-staged kernels (compress_spec_lds_kernel; blocks > 64 KiB parse from
     memory there; threshold raised so every late pass takes them),
-    "speculative-batched" with the batched pass (LZ4M_SPEC_LDS=0)."""
+    "speculative-batched" with the batched pass (LZ4M_SPEC_LDS=0): its
+    17-bit split table for 64 KiB blocks, and for larger blocks the restart
+    with the u32 table; "-u32" the u32 table throughout (LZ4M_SPEC_U17=0)."""
     import lz4._native as N
     from lz4 import _synth
-    monkeypatch.setenv("LZ4M_SPEC_LDS", "0" if mode == "speculative-batched" else "100000")
+    monkeypatch.setenv("LZ4M_SPEC_LDS", "0" if mode.startswith("speculative-batched") else "100000")
+    monkeypatch.setenv("LZ4M_SPEC_U17", "0" if mode.endswith("-u32") else "1")
     m = N.LINKED_SERIAL if mode == "serial" else N.LINKED_SPECULATIVE
     for kind in ("silesia", "text", "records", "runs", "random", "markup"):
         blob = _synth.blocks(48, kind, seed=5).tobytes()
