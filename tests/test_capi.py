@@ -75,6 +75,14 @@ def test_argument_validation_without_gpu():
     assert lib.lz4m_compress_linked_batch(None, None, None, None, None, None, None, None, 4, 1,
                                           N.LINKED_SPECULATIVE, None, 0, None) == N.EINVAL
     assert lib.lz4m_compress_linked_workspace_size(4) >= 4 * 2 * 16384
+    # segmented large-block parse: no-op, bad sizes, missing scratch
+    assert lib.lz4m_pcompress_large_batch(None, None, None, None, None, None, None, 0, 1 << 22, None, 0, None) == 0
+    assert lib.lz4m_pcompress_large_batch(None, None, None, None, None, None, None, -1, 1 << 22, None, 0,
+                                          None) == N.EINVAL
+    assert lib.lz4m_pcompress_large_batch(None, None, None, None, None, None, None, 4, 1 << 22, None, 0,
+                                          None) == N.EINVAL
+    # 16 slots of >= LZ4_compressBound(256 KiB) per block, and 16 per-slot records
+    assert lib.lz4m_pcompress_large_workspace_size(2, 1 << 22) >= 2 * 16 * (N.compress_bound(1 << 18) + 16)
     assert lib.lz4m_xxh32_batch(None, None, None, 0, None, -1, None) == N.EINVAL
     # retired decoder ids (1 lane, 2 coop, 5 direct, 6) and unknown ids are rejected before any launch
     for dec in (1, 2, 5, 6, 8, -1):
