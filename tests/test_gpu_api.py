@@ -450,7 +450,9 @@ def test_frame_compress_device(gpu, reference, parse):
     from lz4 import _synth
     data = _synth.blocks(80, "silesia", seed=9).tobytes()[:5_000_000]
     d = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(gpu)
-    for bs in (lz4.frame.BLOCKSIZE_MAX64KB, lz4.frame.BLOCKSIZE_MAX4MB):
+    # (256 KiB - 4 MiB blocks: the segmented parse of lz4m_pcompress_large_batch with parse="parallel")
+    for bs in (lz4.frame.BLOCKSIZE_MAX64KB, lz4.frame.BLOCKSIZE_MAX256KB, lz4.frame.BLOCKSIZE_MAX1MB,
+               lz4.frame.BLOCKSIZE_MAX4MB):
         f = lz4.frame.compress_device(d, block_size=bs, block_linked=False, content_checksum=True,
                                       block_checksum=(bs == 4), parse=parse).cpu().numpy().tobytes()
         code, out = O.ref_decompress_frame(reference, f)
