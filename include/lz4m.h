@@ -287,7 +287,12 @@ int lz4m_decompress_solo(const uint8_t* d_src, const int64_t* d_src_off, const i
  * that receives the compressed bytes at the end of the launch; d_dst (device
  * memory) receives them instead when h_out is nullptr; h_done: as for
  * lz4m_decompress_solo.
+ * *d_out_len: the compressed size (> 0), 0 (does not fit cap), or
+ * LZ4M_SOLO_STAGE_FAIL (-2): the workgroup gave up waiting for the block to
+ * be staged in LDS (bounded wait) and wrote no bytes -- not a result; redo
+ * the call, e.g. through lz4m_compress_batch (what lz4m_host.hip does).
  */
+#define LZ4M_SOLO_STAGE_FAIL (-2)
 int lz4m_compress_solo(const uint8_t* d_src, int32_t len, uint8_t* d_dst, int32_t cap, int32_t* d_out_len,
                        int table, int acceleration, uint8_t* h_out, int32_t* h_done, lz4m_stream_t stream);
 

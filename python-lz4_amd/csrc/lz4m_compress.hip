@@ -448,7 +448,7 @@ constexpr int32_t kStageChunk = 4096;
 // reports kSoloStageFail instead of the bytes it made (no
 // silently wrong block)
 constexpr int32_t kStageFail = 17;
-constexpr int32_t kSoloStageFail = -2;   // internal result: redo the call another way (lz4m_host.hip)
+constexpr int32_t kSoloStageFail = LZ4M_SOLO_STAGE_FAIL;   // internal result: redo the call another way (lz4m_host.hip)
 typedef __attribute__((address_space(3))) volatile int32_t lds_vi32;
 __device__ __forceinline__ void lw_need(const int32_t* stage, int32_t& have, int32_t x) {
     if (stage == nullptr) return;
@@ -1555,18 +1555,26 @@ extern "C" int lz4m_selftest_lds_order(void) {
     return rc ? -rc : (int)h;
 }
 
-// 0 once the current process's device passed the lane-order self-test, else
-// LZ4M_EDEVICE (the exact compressor would not reproduce the reference's
-// bytes); run once per process, at the first compression
+// 0 once the current device passed the lane-order self-test; LZ4M_EDEVICE
+// once it failed it (the exact compressor would not reproduce the
+// reference's bytes).  Run at a device's first compression.  Only a verdict
+// is kept (per device ordinal): a HIP error while running the test (no
+// memory, a stream capture in progress) is returned as it is, and the next
+// call tries again.
 static int lds_order_check() {
-    static std::once_flag once;
-    static int verdict = 0;
-    std::call_once(once, [] {
+    constexpr int kMaxDev = 64;
+    static std::mutex mu;
+    static int verdict[kMaxDev] = {0};   // 0 untested, 1 passed, 2 failed
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) dev = 0;
+    std::lock_guard<std::mutex> lock(mu);
+    if (verdict[dev] == 0) {
         const int r = lz4m_selftest_lds_order();
-        verdict = r == 0 ? 0 : LZ4M_EDEVICE;
-        if (r != 0) fprintf(stderr, "lz4m: LDS lane-order self-test failed (%d): compression disabled\n", r);
-    });
-    return verdict;
+        if (r < 0) return -r;   // the test did not run: a HIP error, not a verdict
+        verdict[dev] = r == 0 ? 1 : 2;
+        if (r != 0) fprintf(stderr, "lz4m: LDS lane-order self-test failed on device %d (%d): compression disabled\n", dev, r);
+    }
+    return verdict[dev] == 1 ? 0 : LZ4M_EDEVICE;
 }
 
 extern "C" int lz4m_compress_worker_launch(Mailbox* mb, uint8_t* hd, uint8_t* dbuf, uint64_t idle_ticks,

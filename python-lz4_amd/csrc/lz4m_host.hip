@@ -174,7 +174,7 @@ constexpr uint64_t kIdle = 200000;            // 2 ms of the 100 MHz real-time c
 #define LZ4M_WORKER_LIFE 200000               // 2 ms of the 100 MHz clock: a launch's whole lifetime
 #endif
 constexpr uint64_t kLife = LZ4M_WORKER_LIFE;
-constexpr int32_t kSoloStageFail = -2;        // lone-block compress: a staging wait gave up (lz4m_compress.hip)
+constexpr int32_t kSoloStageFail = LZ4M_SOLO_STAGE_FAIL;        // lone-block compress: a staging wait gave up (lz4m_compress.hip)
 
 std::atomic<int> g_worker_mode{-1};           // -1: from LZ4M_WORKER at first use
 // every call the worker path took and then handed to the launch path: a

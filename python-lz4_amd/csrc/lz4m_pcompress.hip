@@ -413,6 +413,13 @@ __host__ __device__ inline int32_t seg_len(int32_t n) {
 }
 // scratch bytes of one segment slot (>= LZ4_compressBound of the segment)
 __host__ __device__ inline int64_t seg_slot(int32_t seg) { return (((int64_t)seg + seg / 255 + 80) + 15) & ~(int64_t)15; }
+// segments of an n-byte block (1..kSegs; non-decreasing in n, so a batch's
+// longest block bounds every block's count)
+__host__ __device__ inline int32_t seg_count(int32_t n) {
+    if (n <= 0) return 1;
+    const int32_t seg = seg_len(n);
+    return (int32_t)(((int64_t)n + seg - 1) / seg);
+}
 
 template <bool BIG, int HB, bool WIN = false, bool SEG = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((BIG && !WIN) || HB > 12 ? 1 : 5))) void pcompress_kernel(const uint8_t* __restrict__ src,
@@ -421,26 +428,29 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((BIG && !WIN
                                                        const int64_t* __restrict__ dst_off,
                                                        const int32_t* __restrict__ dst_cap,
                                                        int32_t* __restrict__ out_len, int64_t n,
-                                                       int32_t* __restrict__ seg_meta = nullptr, int64_t seg_cap = 0) {
+                                                       int32_t* __restrict__ seg_meta = nullptr, int64_t seg_cap = 0,
+                                                       int32_t segs = 1) {
     static_assert(!SEG || (BIG && WIN), "segments are parsed with the windowed table");
     // 8192 hash4 entries: u16 positions (blocks <= 64 KiB) or u32 (BIG)
     constexpr int kWords = (BIG && !WIN) ? (1 << HB) : (1 << HB) / 2;   // table size in u32 words
     __shared__ __attribute__((aligned(16))) uint32_t table[kWords];
     const uint32_t lane = threadIdx.x;
-    const int64_t items = SEG ? n * kSegs : n;
+    const int64_t items = SEG ? n * segs : n;
     for (int64_t b = blockIdx.x; b < items; b += gridDim.x) {
         int32_t N, cap, lo = 0, mlast, matchlimit;
         bool fin = true;
         const uint8_t* s;
         uint8_t* d;
         if (SEG) {
-            const int64_t blk = b / kSegs;
-            const int32_t k = (int32_t)(b % kSegs), NB = src_len[blk];
+            // block blk's segments take slots blk * segs .. + segs - 1 (segs:
+            // the batch's longest block's count)
+            const int64_t blk = b / segs;
+            const int32_t k = (int32_t)(b % segs), NB = src_len[blk];
             const int32_t seg = NB > 0 ? seg_len(NB) : kSegMin;
             const int64_t lo64 = (int64_t)k * seg;
-            if (NB < 0 || seg_slot(seg) > seg_cap || (k > 0 && lo64 >= NB)) {   // no such segment / bad block
-                if (lane == 0)
-                    reinterpret_cast<int4*>(seg_meta)[b] = make_int4(NB < 0 || seg_slot(seg) > seg_cap ? -1 : 0, 0, -1, 0);
+            const bool badb = NB < 0 || seg_slot(seg) > seg_cap || seg_count(NB) > segs;
+            if (badb || (k > 0 && lo64 >= NB)) {   // no such segment / bad block
+                if (lane == 0) reinterpret_cast<int4*>(seg_meta)[b] = make_int4(badb ? -1 : 0, 0, -1, 0);
                 continue;
             }
             lo = (int32_t)lo64;
@@ -652,7 +662,8 @@ __global__ __launch_bounds__(64) void pcompress_stitch_kernel(const uint8_t* __r
                                                               const int32_t* __restrict__ dst_cap,
                                                               int32_t* __restrict__ out_len, int64_t n,
                                                               const uint8_t* __restrict__ slots,
-                                                              const int32_t* __restrict__ seg_meta, int64_t seg_cap) {
+                                                              const int32_t* __restrict__ seg_meta, int64_t seg_cap,
+                                                              int32_t segs) {
     const uint32_t lane = threadIdx.x;
     for (int64_t b = blockIdx.x; b < n; b += gridDim.x) {
         const int32_t NB = src_len[b];
@@ -661,10 +672,10 @@ __global__ __launch_bounds__(64) void pcompress_stitch_kernel(const uint8_t* __r
             continue;
         }
         const int32_t seg = NB > 0 ? seg_len(NB) : kSegMin;
-        const int nseg = NB > 0 ? (int)(((int64_t)NB + seg - 1) / seg) : 1;
+        const int nseg = seg_count(NB);
         int4 m = make_int4(0, 0, -1, 0);
-        if ((int)lane < nseg) m = reinterpret_cast<const int4*>(seg_meta)[b * kSegs + lane];
-        const bool bad = __ballot((int)lane < nseg && m.x < 0) != 0;
+        if ((int)lane < nseg && (int)lane < segs) m = reinterpret_cast<const int4*>(seg_meta)[b * segs + lane];
+        const bool bad = nseg > segs || __ballot((int)lane < nseg && m.x < 0) != 0;
         // c_k: the end anchor of the last segment before k with a sequence
         int32_t c = 0, my_c = 0;
         for (int k = 0; k < nseg; ++k) {
@@ -695,16 +706,19 @@ __global__ __launch_bounds__(64) void pcompress_stitch_kernel(const uint8_t* __r
                 q[x] = (uint8_t)(x == 0 ? tok : x < E ? 255u : (uint32_t)(L - 15 - 255 * (E - 1)));
             wave_copy(q + 1 + E, s + ck, L, lane);
             const int32_t h0 = 1 + ext_len<true>(l0) + l0;   // the slot's own first token, length bytes, literals
-            wave_copy(q + 1 + E + L, slots + (b * kSegs + k) * seg_cap + h0, o - h0, lane);
+            wave_copy(q + 1 + E + L, slots + (b * segs + k) * seg_cap + h0, o - h0, lane);
         }
         if (lane == 0) out_len[b] = total;
     }
 }
 
+// slots per block = the longest block's segment count (1 for
+// blocks up to 256 KiB: ~1x the input, not kSegs x)
 extern "C" size_t lz4m_pcompress_large_workspace_size(int64_t n, int32_t max_len) {
     if (n <= 0 || max_len < 0) return 0;
-    const int64_t meta = (n * kSegs * 16 + 255) & ~(int64_t)255;
-    return (size_t)(meta + n * kSegs * seg_slot(max_len > 0 ? seg_len(max_len) : kSegMin));
+    const int64_t segs = seg_count(max_len);
+    const int64_t meta = (n * segs * 16 + 255) & ~(int64_t)255;
+    return (size_t)(meta + n * segs * seg_slot(max_len > 0 ? seg_len(max_len) : kSegMin));
 }
 
 #ifndef LZ4M_PC_SEGHB
@@ -718,26 +732,27 @@ extern "C" int lz4m_pcompress_large_batch(const uint8_t* d_src, const int64_t* d
     if (n == 0) return 0;
     if (d_work == nullptr || work_bytes < lz4m_pcompress_large_workspace_size(n, max_len)) return LZ4M_EINVAL;
     hipStream_t st = (hipStream_t)stream;
+    const int32_t segs = seg_count(max_len);
     int32_t* meta = (int32_t*)d_work;
-    uint8_t* slots = (uint8_t*)d_work + ((n * kSegs * 16 + 255) & ~(int64_t)255);
+    uint8_t* slots = (uint8_t*)d_work + ((n * segs * 16 + 255) & ~(int64_t)255);
     const int64_t cap = seg_slot(max_len > 0 ? seg_len(max_len) : kSegMin);
     static const int hb = [] {
         const char* e = getenv("LZ4M_PC_SEGHB");   // A/B: 12 or 13
         return e ? atoi(e) : LZ4M_PC_SEGHB;
     }();
-    const int64_t items = n * kSegs;
+    const int64_t items = n * segs;
     const uint32_t grid = (uint32_t)(items < (1ll << 30) ? items : (1ll << 30));
     if (hb == 13)
         hipLaunchKernelGGL((pcompress_kernel<true, 13, true, true>), dim3(grid), dim3(64), 0, st, d_src, d_src_off,
-                           d_src_len, slots, nullptr, nullptr, nullptr, n, meta, cap);
+                           d_src_len, slots, nullptr, nullptr, nullptr, n, meta, cap, segs);
     else
         hipLaunchKernelGGL((pcompress_kernel<true, 12, true, true>), dim3(grid), dim3(64), 0, st, d_src, d_src_off,
-                           d_src_len, slots, nullptr, nullptr, nullptr, n, meta, cap);
+                           d_src_len, slots, nullptr, nullptr, nullptr, n, meta, cap, segs);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return (int)e;
     const uint32_t sgrid = (uint32_t)(n < (1ll << 30) ? n : (1ll << 30));
     hipLaunchKernelGGL(pcompress_stitch_kernel, dim3(sgrid), dim3(64), 0, st, d_src, d_src_off, d_src_len, d_dst,
-                       d_dst_off, d_dst_cap, d_out_len, n, slots, meta, cap);
+                       d_dst_off, d_dst_cap, d_out_len, n, slots, meta, cap, segs);
     return (int)hipGetLastError();
 }
 

@@ -857,14 +857,18 @@ __device__ __forceinline__ void parse_round(PSeq& P, int32_t jj, int32_t r, int3
     const lds_cu32a* xd = (const lds_cu32a*)XS;
     const uint32_t q0 = lq >> 2, q1 = q0 < 7u ? q0 + 1u : 7u;   // (lq = 28: one dword, shift 0)
     const uint32_t dwo = __builtin_amdgcn_alignbyte(xd[q1], xd[q0], lq & 3u);
-    const uint32_t bsh = 8u * ((uint32_t)lit - lq);
+    // (lit > 29: the offset lies past the 32 bytes, `slow` re-reads it: any
+    // shift in 0..31 will do -- a wider one would be undefined)
+    const uint32_t bsh = lit > 28 ? 8u : 0u;
 #elif LZ4M_ROWS_OFFTREE
     // the dword pair at pq selected by a tree on its three index bits (14
     // selects) for every lane, instead of a 16-byte and a 32-byte select chain
     // both computed and selected between
     const uint32_t pq = (uint32_t)(po < 28 ? po : 28);
     const uint32_t dwo = dword32_tree(wa, wb, pq);
-    const uint32_t bsh = 8u * ((uint32_t)po - pq);
+    // (po > 29: past the 32 bytes, `slow` re-reads the offset: any shift in
+    // 0..31 will do -- 8 * (po - pq) would reach 32 and be undefined)
+    const uint32_t bsh = po > 28 ? 8u : 0u;
 #else
     const uint32_t pq = (uint32_t)(po < 28 ? po : 28);
     const uint32_t dwo = lit <= 12 ? window_dword(wa, (uint32_t)po) : dword32(wa, wb, pq);

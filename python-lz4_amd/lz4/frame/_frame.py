@@ -568,7 +568,10 @@ def _decompress_pipelined(mv, info, recs, state, as_bytearray):
         done = True
     finally:
         if hasher is not None and not done:
+            # the thread may still be hashing `out`, freed once the exception
+            # leaves this function: it must have ended first
             hasher.put(None)
+            hasher.join()
         # (on an error too: no copy or launch may still use the buffers freed on return)
         for e in up_ev + down_ev + span_ev:
             if e is not None:

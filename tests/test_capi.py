@@ -83,6 +83,12 @@ def test_argument_validation_without_gpu():
                                           None) == N.EINVAL
     # 16 slots of >= LZ4_compressBound(256 KiB) per block, and 16 per-slot records
     assert lib.lz4m_pcompress_large_workspace_size(2, 1 << 22) >= 2 * 16 * (N.compress_bound(1 << 18) + 16)
+    #  slots per block = the longest block's segment count: 256 KiB
+    # blocks are one segment each, so the scratch is about the input's size
+    n = 4096
+    for size, segs in ((1 << 18, 1), (1 << 20, 4), ((1 << 20) + 1, 5)):
+        ws = lib.lz4m_pcompress_large_workspace_size(n, size)
+        assert n * segs * N.compress_bound(1 << 18) <= ws <= n * segs * (N.compress_bound(1 << 18) + 128) + 256
     assert lib.lz4m_xxh32_batch(None, None, None, 0, None, -1, None) == N.EINVAL
     # retired decoder ids (1 lane, 2 coop, 5 direct, 6) and unknown ids are rejected before any launch
     for dec in (1, 2, 5, 6, 8, -1):
