@@ -112,58 +112,26 @@ __device__ __forceinline__ u32x4 period_pattern(u32x4 w, uint32_t off) {
 // 4 bytes -- replays at ~56 cycles per wave-instruction on gfx950
 // (tools/micro/lds_align.hip; cdna_hip_programming.md Guideline 17), and the
 // decoders' history buffers are read and written at arbitrary byte offsets.
-#ifndef LZ4M_LDS_SKIP
-#define LZ4M_LDS_SKIP 0    // A/B: the last two masked ORs of a put only where some lane needs them
-#endif
-#ifndef LZ4M_LDS_MASKLANES
-#define LZ4M_LDS_MASKLANES 0   // A/B: a put's dwords 1-4 exec-masked to the lanes that reach them (r05x: 0.8 % slower)
-#endif
-#ifndef LZ4M_LDS_ALIGN
-#define LZ4M_LDS_ALIGN 1   // 0 = plain (unaligned) wide accesses; 2 = plain stores for wholly covered dwords
-#endif
-// LZ4M_LDS_ALIGN: history accesses at arbitrary byte offsets made of
-// naturally aligned LDS accesses only.  A 16-byte read is three aligned
-// 8-byte reads and a funnel shift; an exact put of k <= 16 bytes is five
-// ds_mskor_b32 (dst = dst & ~mask | data) on the enclosing aligned dwords --
-// atomic per dword, so neighbouring sequences that share a boundary dword
-// can be written by one instruction -- with the masks from a table by
-// (address & 3, k).
+// So both are made of naturally aligned dword accesses only:
+// - a 16-byte read at any offset is five aligned dwords (two ds_read2_b32 and
+//   one ds_read_b32) and four alignbytes;
+// - an exact put of k <= 16 bytes is five ds_mskor_b32 (dst = dst & ~mask |
+//   data) on the enclosing aligned dwords -- atomic per dword, so
+//   neighbouring sequences that share a boundary dword can be written by one
+//   instruction -- with the masks from a table by (address & 3, k) and each
+//   dword's bytes placed by one v_perm with a per-lane selector (0x0C, a zero
+//   byte, outside the put).
 typedef __attribute__((address_space(3))) volatile uint64_t lds_vu64;
 typedef __attribute__((address_space(3))) const uint32_t lds_cu32;
-__device__ __forceinline__ uint32_t lds_addr(const lds_u8* p) { return (uint32_t)(uintptr_t)p; }
-// LZ4M_LDS_PERM: the shifts of an aligned read / put as v_perm with one
-// selector per lane instead of a select and an alignbyte per dword, and the
-// put's data zeroed outside its bytes by the selector (0x0C) instead of an
-// AND with the mask: 2 VALU per put dword instead of 3; the read is five
-// aligned dwords (two ds_read2_b32 and one ds_read_b32) and four alignbytes
-// instead of three aligned qwords, five selects and four alignbytes
-#ifndef LZ4M_LDS_PERM
-#define LZ4M_LDS_PERM 1
-#endif
 typedef __attribute__((address_space(3))) const uint32_t lds_cu32a __attribute__((aligned(4)));
+__device__ __forceinline__ uint32_t lds_addr(const lds_u8* p) { return (uint32_t)(uintptr_t)p; }
 __device__ __forceinline__ u32x4 lds_ld16a(const lds_u8* p) {
-#if LZ4M_LDS_PERM
-    {
-        const uint32_t a = lds_addr(p), r = a & 3u;
-        const lds_cu32a* q = (const lds_cu32a*)(p - r);
-        const uint32_t c0 = q[0], c1 = q[1], c2 = q[2], c3 = q[3], c4 = q[4];
-        return u32x4{__builtin_amdgcn_alignbyte(c1, c0, r), __builtin_amdgcn_alignbyte(c2, c1, r),
-                     __builtin_amdgcn_alignbyte(c3, c2, r), __builtin_amdgcn_alignbyte(c4, c3, r)};
-    }
-#endif
-    const uint32_t a = lds_addr(p);
-    const lds_vu64* q = (const lds_vu64*)(p - (a & 7u));
-    const uint64_t x0 = q[0], x1 = q[1], x2 = q[2];
-    const bool h = (a & 4u) != 0;
-    const uint32_t r = a & 3u;
-    const uint32_t c0 = (uint32_t)x0, c1 = (uint32_t)(x0 >> 32), c2 = (uint32_t)x1, c3 = (uint32_t)(x1 >> 32),
-                   c4 = (uint32_t)x2, c5 = (uint32_t)(x2 >> 32);
-    const uint32_t e0 = h ? c1 : c0, e1 = h ? c2 : c1, e2 = h ? c3 : c2, e3 = h ? c4 : c3, e4 = h ? c5 : c4;
-    return u32x4{__builtin_amdgcn_alignbyte(e1, e0, r), __builtin_amdgcn_alignbyte(e2, e1, r),
-                 __builtin_amdgcn_alignbyte(e3, e2, r), __builtin_amdgcn_alignbyte(e4, e3, r)};
+    const uint32_t a = lds_addr(p), r = a & 3u;
+    const lds_cu32a* q = (const lds_cu32a*)(p - r);
+    const uint32_t c0 = q[0], c1 = q[1], c2 = q[2], c3 = q[3], c4 = q[4];
+    return u32x4{__builtin_amdgcn_alignbyte(c1, c0, r), __builtin_amdgcn_alignbyte(c2, c1, r),
+                 __builtin_amdgcn_alignbyte(c3, c2, r), __builtin_amdgcn_alignbyte(c4, c3, r)};
 }
-#define LZ4M_MSKOR(addr, off, m, x) \
-    asm volatile("ds_mskor_b32 %0, %1, %2 offset:" #off ::"v"(addr), "v"(m), "v"((x) & (m)) : "memory")
 // byte masks of an exact put of k (0..16) bytes at address & 3 == r over the
 // enclosing dwords 0..3: table entry (r * 17 + k), 16 bytes (dword 4 is
 // computed); built once per workgroup by lds_put_table_init
@@ -179,83 +147,31 @@ __device__ __forceinline__ void lds_put_table_init(uint32_t* tab, uint32_t lane,
         tab[e] = m;
     }
 }
+// Exactly k bytes (k >= 16: 16) of v at LDS address p.
 __device__ __forceinline__ void lds_put_al(lds_u8* p, u32x4 v, int32_t k, lds_cu32* tab) {
     const uint32_t a = lds_addr(p), r = a & 3u;
     const uint32_t kk = k >= 16 ? 16u : (uint32_t)k;
-#if LZ4M_LDS_PERM && LZ4M_LDS_ALIGN == 1
-    {
-        // destination dword i, byte b holds put byte 4i + b - r: v_perm of
-        // (v[i], v[i-1]) with selector byte 4 + b - r, 0x0C (zero) where the
-        // mask says the byte is not the put's
-        u32x4 m;
-        __builtin_memcpy(&m, (const uint8_t*)(tab + 4u * (r * 17u + kk)), 16);   // 16-byte aligned
-        const int32_t t4 = (int32_t)(r + kk) - 16;   // bytes in dword 4 (0..3)
-        const uint32_t m4 = t4 > 0 ? (1u << (8 * t4)) - 1u : 0u;
-        // r replicated into every byte by one v_perm (a v_mul_lo_u32 is quarter rate)
-        const uint32_t sb = 0x07060504u - __builtin_amdgcn_perm(0u, r, 0u);
-        const uint32_t b4 = a & ~3u;
-        auto sel = [&](uint32_t mk) __attribute__((always_inline)) { return (mk & sb) | (~mk & 0x0C0C0C0Cu); };
-        const uint32_t d0 = __builtin_amdgcn_perm(v.x, v.x, sel(m.x));
-        const uint32_t d1 = __builtin_amdgcn_perm(v.y, v.x, sel(m.y));
-        const uint32_t d2 = __builtin_amdgcn_perm(v.z, v.y, sel(m.z));
-        const uint32_t d3 = __builtin_amdgcn_perm(v.w, v.z, sel(m.w));
-        const uint32_t d4 = __builtin_amdgcn_perm(0u, v.w, sel(m4));
-        asm volatile("ds_mskor_b32 %0, %1, %2 offset:0" ::"v"(b4), "v"(m.x), "v"(d0) : "memory");
-#if LZ4M_LDS_MASKLANES
-        // dwords 1-4 only in the lanes whose put reaches them (an LDS access
-        // costs per active lane)
-        if (m.y) asm volatile("ds_mskor_b32 %0, %1, %2 offset:4" ::"v"(b4), "v"(m.y), "v"(d1) : "memory");
-        if (m.z) asm volatile("ds_mskor_b32 %0, %1, %2 offset:8" ::"v"(b4), "v"(m.z), "v"(d2) : "memory");
-        if (m.w) asm volatile("ds_mskor_b32 %0, %1, %2 offset:12" ::"v"(b4), "v"(m.w), "v"(d3) : "memory");
-        if (m4) asm volatile("ds_mskor_b32 %0, %1, %2 offset:16" ::"v"(b4), "v"(m4), "v"(d4) : "memory");
-#else
-        asm volatile("ds_mskor_b32 %0, %1, %2 offset:4" ::"v"(b4), "v"(m.y), "v"(d1) : "memory");
-        asm volatile("ds_mskor_b32 %0, %1, %2 offset:8" ::"v"(b4), "v"(m.z), "v"(d2) : "memory");
-        if (!LZ4M_LDS_SKIP || __any(m.w != 0u))
-            asm volatile("ds_mskor_b32 %0, %1, %2 offset:12" ::"v"(b4), "v"(m.w), "v"(d3) : "memory");
-        if (!LZ4M_LDS_SKIP || __any(m4 != 0u))
-            asm volatile("ds_mskor_b32 %0, %1, %2 offset:16" ::"v"(b4), "v"(m4), "v"(d4) : "memory");
-#endif
-        return;
-    }
-#endif
-    const uint32_t s = (4u - r) & 3u;
-    const bool z = r == 0;
-    const uint32_t d0 = __builtin_amdgcn_alignbyte(v.x, z ? v.x : 0u, s);
-    const uint32_t d1 = __builtin_amdgcn_alignbyte(v.y, z ? v.y : v.x, s);
-    const uint32_t d2 = __builtin_amdgcn_alignbyte(v.z, z ? v.z : v.y, s);
-    const uint32_t d3 = __builtin_amdgcn_alignbyte(v.w, z ? v.w : v.z, s);
-    const uint32_t d4 = __builtin_amdgcn_alignbyte(0u, z ? 0u : v.w, s);
+    // destination dword i, byte b holds put byte 4i + b - r: v_perm of
+    // (v[i], v[i-1]) with selector byte 4 + b - r, 0x0C (zero) where the
+    // mask says the byte is not the put's
     u32x4 m;
     __builtin_memcpy(&m, (const uint8_t*)(tab + 4u * (r * 17u + kk)), 16);   // 16-byte aligned
     const int32_t t4 = (int32_t)(r + kk) - 16;   // bytes in dword 4 (0..3)
     const uint32_t m4 = t4 > 0 ? (1u << (8 * t4)) - 1u : 0u;
+    // r replicated into every byte by one v_perm (a v_mul_lo_u32 is quarter rate)
+    const uint32_t sb = 0x07060504u - __builtin_amdgcn_perm(0u, r, 0u);
     const uint32_t b4 = a & ~3u;
-#if LZ4M_LDS_ALIGN >= 2
-    // a dword the put covers wholly is owned by this lane: a plain aligned
-    // store (about half a masked OR's LDS time); partial ones are masked ORs
-    lds_u8* q = p - r;
-    typedef __attribute__((address_space(3))) volatile uint32_t vu32;
-    if (m.x == ~0u) { *(vu32*)q = d0; } else if (m.x) { LZ4M_MSKOR(b4, 0, m.x, d0); }
-    if (m.y == ~0u) { *(vu32*)(q + 4) = d1; } else if (m.y) { LZ4M_MSKOR(b4, 4, m.y, d1); }
-    if (m.z == ~0u) { *(vu32*)(q + 8) = d2; } else if (m.z) { LZ4M_MSKOR(b4, 8, m.z, d2); }
-    if (m.w == ~0u) { *(vu32*)(q + 12) = d3; } else if (m.w) { LZ4M_MSKOR(b4, 12, m.w, d3); }
-    if (m4) LZ4M_MSKOR(b4, 16, m4, d4);
-#elif LZ4M_LDS_SKIP
-    // dwords 3 and 4 hold bytes only for puts reaching past byte 12 of the
-    // span (kk > 12 - r): skipped where no lane of the wave needs them
-    LZ4M_MSKOR(b4, 0, m.x, d0);
-    LZ4M_MSKOR(b4, 4, m.y, d1);
-    LZ4M_MSKOR(b4, 8, m.z, d2);
-    if (m.w) LZ4M_MSKOR(b4, 12, m.w, d3);
-    if (m4) LZ4M_MSKOR(b4, 16, m4, d4);
-#else
-    LZ4M_MSKOR(b4, 0, m.x, d0);
-    LZ4M_MSKOR(b4, 4, m.y, d1);
-    LZ4M_MSKOR(b4, 8, m.z, d2);
-    LZ4M_MSKOR(b4, 12, m.w, d3);
-    LZ4M_MSKOR(b4, 16, m4, d4);
-#endif
+    auto sel = [&](uint32_t mk) __attribute__((always_inline)) { return (mk & sb) | (~mk & 0x0C0C0C0Cu); };
+    const uint32_t d0 = __builtin_amdgcn_perm(v.x, v.x, sel(m.x));
+    const uint32_t d1 = __builtin_amdgcn_perm(v.y, v.x, sel(m.y));
+    const uint32_t d2 = __builtin_amdgcn_perm(v.z, v.y, sel(m.z));
+    const uint32_t d3 = __builtin_amdgcn_perm(v.w, v.z, sel(m.w));
+    const uint32_t d4 = __builtin_amdgcn_perm(0u, v.w, sel(m4));
+    asm volatile("ds_mskor_b32 %0, %1, %2 offset:0" ::"v"(b4), "v"(m.x), "v"(d0) : "memory");
+    asm volatile("ds_mskor_b32 %0, %1, %2 offset:4" ::"v"(b4), "v"(m.y), "v"(d1) : "memory");
+    asm volatile("ds_mskor_b32 %0, %1, %2 offset:8" ::"v"(b4), "v"(m.z), "v"(d2) : "memory");
+    asm volatile("ds_mskor_b32 %0, %1, %2 offset:12" ::"v"(b4), "v"(m.w), "v"(d3) : "memory");
+    asm volatile("ds_mskor_b32 %0, %1, %2 offset:16" ::"v"(b4), "v"(m4), "v"(d4) : "memory");
 }
 
 // ------------------------------------------------ period-pattern selectors

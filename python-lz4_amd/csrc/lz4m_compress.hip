@@ -38,21 +38,6 @@ int pcompress_launch(const uint8_t* d_src, const int64_t* d_src_off, const int32
                      const int64_t* d_dst_off, const int32_t* d_dst_cap, int32_t* d_out_len, int64_t n, int variant,
                      hipStream_t stream);
 
-// Diagnostic build only (-DLZ4M_COMPRESS_PROF): wave-cycle sums per phase of
-// compress_block_w and event counts, read with lz4m_compress_prof.
-#ifdef LZ4M_COMPRESS_PROF
-__device__ unsigned long long g_cprof[32];
-#define CP_DECL uint64_t cp[16] = {0}; uint64_t cp_t = clock64();
-#define CP_MARK(i) do { const uint64_t _t = clock64(); cp[i] += _t - cp_t; cp_t = _t; } while (0)
-#define CP_COUNT(i, x) cp[i] += (uint64_t)(x)
-#define CP_FLUSH() do { if (lane == 0) for (int _i = 0; _i < 16; ++_i) atomicAdd(&g_cprof[_i], (unsigned long long)cp[_i]); } while (0)
-#else
-#define CP_DECL
-#define CP_MARK(i) do {} while (0)
-#define CP_COUNT(i, x) do {} while (0)
-#define CP_FLUSH() do {} while (0)
-#endif
-
 constexpr int kMinLength = 13;        // lz4.c:247
 constexpr int kLimit64K = 65536 + 11; // lz4.c:689
 constexpr int kMaxInput = 0x7E000000; // lz4.h:211
@@ -175,7 +160,7 @@ struct Table<kTableU17> {
     }
 };
 
-// LZ4M_CMP_XCHG: the search step inserts its 64 positions with one LDS
+// The search step inserts its 64 positions with one LDS
 // exchange per lane; lanes of a wave that hit the same bucket are applied in
 // lane order (gfx950: every one of 33.5 M instructions of random collision
 // patterns, tools/micro/lds_xchg_order.hip, r05l), so each lane reads back
@@ -185,9 +170,6 @@ struct Table<kTableU17> {
 // back what it read (positions increase with the lane, so that lane is the one
 // whose read value is below lane f+1's position).  Replaces a read, a probe
 // write, a read back and a loop over the colliding groups.
-#ifndef LZ4M_CMP_XCHG
-#define LZ4M_CMP_XCHG 1
-#endif
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 __device__ __forceinline__ int64_t uni64(int64_t v) {
@@ -233,14 +215,7 @@ __device__ __forceinline__ void gbl_put_c(uint8_t* p, u32x4 v, int32_t k) {
     for (int32_t j = 0; j < k; ++j) p[j] = (uint8_t)byte_of(v, j);
 }
 
-// LZ4M_COMPRESS_XP (timing probes only, WRONG output): bit 1 = the parse
-// issues no store of its output (compress_block_w), to measure what the
-// stores' place in the in-order memory counter costs the serial parse
-#ifndef LZ4M_COMPRESS_XP
-#define LZ4M_COMPRESS_XP 0
-#endif
-#define CST(stmt) do { if (!(LZ4M_COMPRESS_XP & 1)) { stmt; } } while (0)
-// LZ4M_CMP_TNMERGE: at acceleration 1 the test of the next position after a
+// kTnMerge: at acceleration 1 the test of the next position after a
 // match (lz4.c:1207-1258) may be lane 0 of the next search step instead of a
 // step of its own.  Exact: it is the search attempt at ip with anchor == ip
 // (no catch-up, no literals), after the insert of ip - 2; the step's other
@@ -249,20 +224,18 @@ __device__ __forceinline__ void gbl_put_c(uint8_t* p, u32x4 v, int32_t k) {
 // by the match's, lz4.c:1085-1089 vs 1184-1190).  A 64-lane step costs more
 // than the lone test, so this pays only where the test mostly fails: the
 // parse keeps a running hit rate of the test (1/256 units, weight 1/8) and
-// merges while it is below LZ4M_CMP_TNMERGE (0: never; 257: always).  r05h:
+// merges while it is below kTnMerge (0: never; 257: always).  r05h:
 // always merging cost silesia-like / text blocks 10 / 30 % and saved 13 % on
 // binary records; r05i, against never: threshold 64 -5.5 % silesia-like,
 // +2.4 % text, -12 % records (96: -5.0 / +3.4 / -12; 128: -3.5 / +8.5 / -12).
-#ifndef LZ4M_CMP_TNMERGE
-#define LZ4M_CMP_TNMERGE 64
-#endif
+constexpr int32_t kTnMerge = 64;
 
 // length bytes after a token nibble of 15 (lz4.c:1094-1099, 1184-1194);
 // returns the new output position.  Written by lane 0.
 __device__ __forceinline__ int64_t put_len(uint8_t* dst, int64_t op, int64_t len, uint32_t lane) {
     const int64_t n255 = len / 255;
-    for (int64_t k = lane; k < n255; k += kWave) CST(dst[op + k] = 255);
-    if (lane == 0) CST(dst[op + n255] = (uint8_t)(len - 255 * n255));
+    for (int64_t k = lane; k < n255; k += kWave) dst[op + k] = 255;
+    if (lane == 0) dst[op + n255] = (uint8_t)(len - 255 * n255);
     return op + n255 + 1;
 }
 
@@ -273,43 +246,16 @@ __device__ __forceinline__ int64_t put_len(uint8_t* dst, int64_t op, int64_t len
 // reads; only the candidate side (anywhere in the last 64 KiB) is read from
 // HBM / L2, 20 bytes per candidate, which settles the 4-byte check, a short
 // catch-up and a short match in one round trip.
-#ifndef LZ4M_CRING
-#define LZ4M_CRING 1024
-#endif
-constexpr int kRing = LZ4M_CRING;
-#ifndef LZ4M_CCHUNK
-#define LZ4M_CCHUNK 512
-#endif
-constexpr int kChunk = LZ4M_CCHUNK;      // refill unit: 16 or 8 bytes per lane
+constexpr int kRing = 1024;
+constexpr int kChunk = 512;   // refill unit: 8 bytes per lane
 constexpr int kLaneB = kChunk / kWave;
 static_assert(kLaneB == 16 || kLaneB == 8, "ring refill granularity");
 static_assert(kChunk <= kRing / 2, "ring too small for its refill unit");
-#ifdef LZ4M_NO_RING
-constexpr int kRingBytes = 16;           // A/B builds: every source read from memory
-#else
 constexpr int kRingBytes = kRing + 32;   // + a mirror of the first 32 bytes
-#endif
-// LZ4M_CMP_STAGE: bytes of LDS output staging after the ring (0: none; 448
-// fits the LDS allocation the table and the ring already take, 9 waves per
-// CU).  r05h: 2-4 % slower on silesia-like / text blocks, 1 % faster on
-// binary records -- the parse's stores cost their issue, not waits (off)
-#ifndef LZ4M_CMP_STAGE
-#define LZ4M_CMP_STAGE 0
-#endif
-#ifdef LZ4M_NO_RING
-constexpr int kOB = 0;
-#else
-constexpr int kOB = LZ4M_CMP_STAGE;
-#endif
-static_assert(kOB % 16 == 0 && kOB < 16 * kWave, "staging: whole 16-byte pieces, one per lane");
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
-#ifdef LZ4M_NO_RING   // A/B: no ring in LDS at all (the 16 KiB table alone, 10 waves per CU)
-#define RING_DECL lds_u8* ring = nullptr;
-#else
 #define RING_DECL                                                               \
-    __shared__ __attribute__((aligned(16))) uint8_t ring_mem[kRingBytes + kOB];   \
+    __shared__ __attribute__((aligned(16))) uint8_t ring_mem[kRingBytes];         \
     lds_u8* ring = (lds_u8*)ring_mem;
-#endif
 
 struct Win {
     lds_u8* r;
@@ -317,20 +263,12 @@ struct Win {
     int32_t whi;    // resident: [max(base, whi - kRing), whi)
     int32_t iend;
     __device__ __forceinline__ bool has(int32_t p, int32_t len) const {
-#ifdef LZ4M_NO_RING
-        return false;
-#endif
         return p >= base && p >= whi - kRing && p + len <= whi;
     }
 };
 
 // bytes [p-4, p) -> pm and [p, p+16) -> v from the ring (p resident per has(p-4, 20))
 __device__ __forceinline__ void ring_fetch(const Win& W, int32_t p, uint32_t& pm, u32x4& v) {
-#ifdef LZ4M_NO_RING
-    pm = 0;
-    v = u32x4{0, 0, 0, 0};
-    return;
-#endif
     const uint32_t i = (uint32_t)(p - W.base) & (kRing - 1);
     const uint32_t sh = i & 3, j = i >> 2;
     const lds_u32* R = (const lds_u32*)W.r;
@@ -342,9 +280,6 @@ __device__ __forceinline__ void ring_fetch(const Win& W, int32_t p, uint32_t& pm
 }
 
 __device__ __forceinline__ u32x4 ring_fetch16(const Win& W, int32_t p) {
-#ifdef LZ4M_NO_RING
-    return u32x4{0, 0, 0, 0};
-#endif
     const uint32_t i = (uint32_t)(p - W.base) & (kRing - 1);
     const uint32_t sh = i & 3, j = i >> 2;
     const lds_u32* R = (const lds_u32*)W.r;
@@ -355,9 +290,6 @@ __device__ __forceinline__ u32x4 ring_fetch16(const Win& W, int32_t p) {
 
 // a refill may overwrite ring bytes that are before `keep` (or before the block)
 __device__ __forceinline__ bool can_fill(const Win& W, int32_t keep) {
-#ifdef LZ4M_NO_RING
-    return false;
-#endif
     return W.whi < W.iend && W.whi - kRing + kChunk <= (keep > W.base ? keep : W.base);
 }
 // bytes [p, p+16) of the window for 0 <= p < iend; bytes at or past iend are
@@ -528,21 +460,8 @@ __device__ __forceinline__ int32_t compress_block_w(const uint8_t* __restrict__ 
     int32_t pbase = 0, gbase = 0, back = 0;
 
     int32_t staged = 0;   // LW with `stage`: bytes known to be in LDS (wave uniform)
-    int32_t tnb = 0;      // 1: the next search step starts with the test of position ip (LZ4M_CMP_TNMERGE)
+    int32_t tnb = 0;      // 1: the next search step starts with the test of position ip (kTnMerge)
     int32_t tnh = 128;    // running hit rate of the test of the next position, 1/256 units
-    // output staging (LZ4M_CMP_STAGE): output bytes [fbase, op) wait in LDS and
-    // leave in one coalesced store per lane, so that the parse's loads seldom
-    // wait for its own stores (gfx9 counts both in one in-order counter)
-    constexpr bool kStg = !LW && (LZ4M_CMP_STAGE > 0);
-    lds_u8* const ob = kStg ? ring + kRingBytes : nullptr;
-    int32_t fbase = 0;
-    auto ob_flush = [&]() __attribute__((always_inline)) {
-        const int32_t pend = op - fbase;
-        const int32_t c = 16 * (int32_t)lane;
-        if (c < pend) CST(gbl_put_c(dst + fbase + c, lds_ld16(ob + c), pend - c));
-        fbase = op;
-    };
-    CP_DECL
     if (n < kMinLength) goto last_literals;                    // lz4.c:981
 
     if constexpr (!LW) top_up(W, w, hist + kRing, hist, lane);
@@ -583,53 +502,23 @@ __device__ __forceinline__ int32_t compress_block_w(const uint8_t* __restrict__ 
                     }
                     src_fetch(W, w, pos, pm, pv);
                 }
-                CP_COUNT(8, 1);
-                CP_COUNT(15, __builtin_popcountll(__ballot(valid && !W.has(pos - 4, 20))));
                 const uint32_t cur = ibase + (uint32_t)pos;
-                // read the bucket, then probe it with the lane id: a lane that
-                // does not read its own id back shares its hash with another
-                // lane of this step (one LDS round trip, in order per wave)
-                uint32_t h = 0, old = 0, rb = lane;
+                // each lane exchanges its position into its bucket (one LDS
+                // round trip; the lanes of a bucket in lane order, below)
+                uint32_t h = 0, old = 0;
                 if (tnb && k0 == 0 && lane == 0) {   // lz4.c:1207-1208: ip - 2 first
                     const u32x4 pv2 = u32x4{__builtin_amdgcn_alignbyte(pv.x, pm, 2),
                                             __builtin_amdgcn_alignbyte(pv.y, pv.x, 2), 0u, 0u};
                     T::put_v(tab, T::hash_v(pv2), cur - 2u);
                 }
-                if (LZ4M_CMP_XCHG) {
-                    if (valid) {
-                        h = T::hash_v(pv);
-                        old = T::xchg(tab, h, cur);
-                    }
-                } else if (valid) {
+                if (valid) {
                     h = T::hash_v(pv);
-                    old = T::get_v(tab, h);
-                    T::put_v(tab, h, lane);
-                    rb = T::get_v(tab, h);
+                    old = T::xchg(tab, h, cur);
                 }
-                CP_MARK(0);
-                // per hash group: nearest earlier (pred) and later (succ) lane
-                int pred = -1, succ = 1 << 20;
-                uint64_t todo = LZ4M_CMP_XCHG ? 0ull : __ballot(rb != lane);
-                while (todo) {
-                    CP_COUNT(11, 1);
-                    const int l = __builtin_ctzll(todo);
-                    const uint32_t h0 = (uint32_t)__builtin_amdgcn_readlane((int)h, l);
-                    const bool in = valid && h == h0;
-                    const uint64_t same = __ballot(in);
-                    todo &= ~same;
-                    if (in) {
-                        const uint64_t lt = same & ((1ull << lane) - 1ull);
-                        const uint64_t gt = lane == 63 ? 0ull : same & ~((2ull << lane) - 1ull);
-                        pred = lt ? 63 - __builtin_clzll(lt) : -1;
-                        succ = gt ? __builtin_ctzll(gt) : 1 << 20;
-                    }
-                }
-                CP_MARK(1);
-                // the serial loop inserted an earlier lane of the group first
-                const uint32_t cand =
-                    pred >= 0 ? ibase + (uint32_t)(ipo + (unit ? (SI)pred - (SI)tnb
-                                                               : attempt_off<SI>(k0 + (SI)pred - (SI)tnb, A, FA)))
-                              : old;
+                // the exchange returns to each lane what the serial insert
+                // order reads: the previous lane's position of its bucket, or
+                // the table's entry for the bucket's first lane
+                const uint32_t cand = old;
                 int32_t cpos = pos;
                 bool ok = false;
                 u32x4 gv = u32x4{0, 0, 0, 0};
@@ -650,20 +539,13 @@ __device__ __forceinline__ int32_t compress_block_w(const uint8_t* __restrict__ 
                 const bool hit = ok && gv.x == pv.x;
                 const uint64_t hmask = __ballot(hit);
                 const int f = hmask ? __builtin_ctzll(hmask) : nvalid;   // last lane processed: f (or all valid)
-                if (LZ4M_CMP_TNMERGE > 0 && tnb && k0 == 0) tnh += ((int32_t)(hmask & 1u) * 256 - tnh) >> 3;
-                if (LZ4M_CMP_XCHG) {
-                    // undo the lanes after f: the first of each bucket restores
-                    if (f < nvalid) {
-                        const uint32_t cf1 = (uint32_t)__builtin_amdgcn_readlane((int)cur, f < 63 ? f + 1 : 63);
-                        if (valid && (int)lane > f && old < cf1) T::put_v(tab, h, old);
-                    }
-                } else if (valid && (((int)lane <= f && succ > f) || ((int)lane > f && pred < 0))) {
-                    // one write per touched bucket: the group's last lane <= f
-                    // inserts its position; a group entirely after f restores
-                    T::put_v(tab, h, (int)lane <= f ? cur : old);
+                if (tnb && k0 == 0) tnh += ((int32_t)(hmask & 1u) * 256 - tnh) >> 3;
+                // undo the lanes after f: the first of each bucket restores
+                if (f < nvalid) {
+                    const uint32_t cf1 = (uint32_t)__builtin_amdgcn_readlane((int)cur, f < 63 ? f + 1 : 63);
+                    if (valid && (int)lane > f && old < cf1) T::put_v(tab, h, old);
                 }
                 if (pf) fill_commit(W, fv, lane);
-                CP_MARK(2);
                 if (hmask) {
                     ip = __builtin_amdgcn_readlane(pos, f);
                     match = __builtin_amdgcn_readlane(cpos, f);
@@ -689,7 +571,6 @@ __device__ __forceinline__ int32_t compress_block_w(const uint8_t* __restrict__ 
             ip -= r;
             match -= r;
             if (r == 4 && lim > 4) {
-                CP_COUNT(13, 1);
                 for (;;) {
                     const int32_t a = ip - 1 - lane, b = match - 1 - lane;
                     const bool okc = a >= anchor && b >= low && w[a < 0 ? 0 : a] == w[b < 0 ? 0 : b];
@@ -701,8 +582,6 @@ __device__ __forceinline__ int32_t compress_block_w(const uint8_t* __restrict__ 
                 }
             }
             back = pbase - ip;
-            CP_MARK(3);
-            CP_COUNT(9, 1);
         }
 
     next_match:   // (the separate test of the next position: anchor == ip, no literals)
@@ -758,59 +637,16 @@ __device__ __forceinline__ int32_t compress_block_w(const uint8_t* __restrict__ 
                     break;
                 }
                 mcode += more;
-                CP_COUNT(12, 1);
             }
             mcode = (int32_t)uni((uint32_t)mcode);
-            CP_MARK(5);
             // the output checks, in the reference's order (lz4.c:1085-1089, 1184-1190;
             // for the test of the next position the first is implied by the second)
             if (limited && op + 1 + lit + (2 + 1 + 5) + lit / 255 > cap) return 0;
             const int32_t llb = lit >= 15 ? (lit - 15) / 255 + 1 : 0;   // literal-length bytes
             const int32_t mlb = mcode >= 15 ? (mcode - 15) / 255 + 1 : 0;   // match-length bytes
             if (limited && op + 1 + llb + lit + 2 + (1 + 5) + (mcode + 240) / 255 > cap) return 0;
-            const int32_t size = 1 + llb + lit + 2 + mlb;
             const uint32_t tok = ((uint32_t)(lit < 15 ? lit : 15) << 4) | (uint32_t)(mcode < 15 ? mcode : 15);
-            if constexpr (kStg) {
-                if (op - fbase + size + 16 > kOB) ob_flush();   // at a sequence boundary
-            }
-            if (kStg && size + 16 <= kOB) {
-                // into the staging buffer: every write lands before [op - fbase + size + 16)
-                lds_u8* const o = ob + (op - fbase);
-                if (lane == 0) o[0] = (uint8_t)tok;
-                int32_t x = 1;
-                if (llb) {
-                    const int32_t n255 = llb - 1;
-                    for (int32_t k = lane; k < n255; k += kWave) o[1 + k] = 255;
-                    if (lane == 0) o[1 + n255] = (uint8_t)(lit - 15 - 255 * n255);
-                    x += llb;
-                }
-                {   // whole 16-byte pieces (the spill past the literal is overwritten below)
-                    const int32_t q = 16 * (int32_t)lane;
-                    if (q < lit) {
-                        const int32_t p = anchor + q;
-                        const bool in = W.has(p, 16);
-                        u32x4 v = ring_fetch16(W, p);
-                        if (__any(!in)) {
-                            const u32x4 gv = ld16_win(w, p, iend);
-                            if (!in) v = gv;
-                        }
-                        lds_st16(o + x + q, v);
-                    }
-                }
-                x += lit;
-                if (lane == 0) {
-                    o[x] = (uint8_t)off;
-                    o[x + 1] = (uint8_t)(off >> 8);
-                }
-                x += 2;
-                if (mlb) {
-                    const int32_t n255 = mlb - 1;
-                    for (int32_t k = lane; k < n255; k += kWave) o[x + k] = 255;
-                    if (lane == 0) o[x + n255] = (uint8_t)(mcode - 15 - 255 * n255);
-                }
-                op += size;
-            } else {
-                // straight to dst (a sequence larger than the staging buffer, or LW)
+            {
                 const int32_t tok_pos = op;
                 op += 1;
                 if (llb) op = put_len(dst, op, lit - 15, lane);
@@ -832,28 +668,26 @@ __device__ __forceinline__ int32_t compress_block_w(const uint8_t* __restrict__ 
                             }
                         }
                         if (lit - q >= 16 || d_room - q >= 16) {
-                            CST(st16(d + q, v));
+                            st16(d + q, v);
                         } else {
-                            for (int32_t j = 0; j < lit - q; ++j) CST(d[q + j] = (uint8_t)byte_of(v, (int)j));
+                            for (int32_t j = 0; j < lit - q; ++j) d[q + j] = (uint8_t)byte_of(v, (int)j);
                         }
                     }
                 }
                 op += lit;
                 if (lane == 0) {
-                    CST(dst[op] = (uint8_t)off);
-                    CST(dst[op + 1] = (uint8_t)(off >> 8));
+                    dst[op] = (uint8_t)off;
+                    dst[op + 1] = (uint8_t)(off >> 8);
                 }
                 op += 2;
                 if (mlb) op = put_len(dst, op, mcode - 15, lane);
-                if (lane == 0) CST(dst[tok_pos] = (uint8_t)tok);
-                if constexpr (kStg) fbase = op;
+                if (lane == 0) dst[tok_pos] = (uint8_t)tok;
             }
             ip += mcode + 4;
-            CP_MARK(4);
         }
         anchor = ip;
         if (ip >= mflimit1) break;                             // lz4.c:1204
-        tnb = LZ4M_CMP_TNMERGE > 0 && A == 64 && tnh < LZ4M_CMP_TNMERGE;
+        tnb = A == 64 && tnh < kTnMerge;
         if (tnb) continue;   // the test of ip: lane 0 of the next search step
 
         {   // ---- fill table, test next position (lz4.c:1207-1258) ----
@@ -882,7 +716,7 @@ __device__ __forceinline__ int32_t compress_block_w(const uint8_t* __restrict__ 
                 // (a candidate inside the ring read from there instead: -0.5 %, r04aa)
                 const u32x4 gv = LW ? lw_ld16(w, cpos) : ld16_win(w, cpos, iend);
                 const bool thit = ok && gv.x == pv.x;
-                if (LZ4M_CMP_TNMERGE > 0) tnh += ((int32_t)thit * 256 - tnh) >> 3;
+                tnh += ((int32_t)thit * 256 - tnh) >> 3;
                 if (thit) {
                     match = cpos;
                     P = pv;
@@ -890,18 +724,14 @@ __device__ __forceinline__ int32_t compress_block_w(const uint8_t* __restrict__ 
                     pbase = ip;
                     gbase = cpos;
                     back = 0;
-                    CP_MARK(6);
-                    CP_COUNT(10, 1);
                     goto next_match;
                 }
             }
-            CP_MARK(6);
         }
         ++ip;
     }
 
 last_literals:
-    if constexpr (kStg) ob_flush();
     {   // lz4.c:1266-1293
         const int32_t run = iend - anchor;
         if (limited && op + run + 1 + (run + 255 - 15) / 255 > cap) return 0;
@@ -923,8 +753,6 @@ last_literals:
         }
         op += run;
     }
-    CP_MARK(7);
-    CP_FLUSH();
     return op;
 }
 
@@ -1495,7 +1323,7 @@ __global__ __launch_bounds__(256) void compress_worker(Mailbox* mb, uint8_t* hd,
     }
 }
 
-// ---- the lane-order self-test (LZ4M_CMP_XCHG, LZ4M_PC_XCHG rest on it) ----
+// ---- the lane-order self-test (the search step's exchange rests on it) ----
 // Every wave runs 64 instructions of each exchange form the compressors use
 // (ds_wrxchg_rtn_b32 on 32-bit entries, ds_mskor_rtn_b32 on 16-bit halves)
 // with pseudo-random bucket collisions, and counts the instructions whose
@@ -1698,18 +1526,9 @@ extern "C" int lz4m_compress_prefix_batch(const uint8_t* d_src, const int64_t* d
 }
 
 extern "C" int lz4m_compress_prof(unsigned long long* out, int reset) {
-#ifdef LZ4M_COMPRESS_PROF
-    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(lz4m::g_cprof), sizeof(unsigned long long) * 16);
-    if (e == hipSuccess && reset) {
-        unsigned long long z[32] = {0};
-        e = hipMemcpyToSymbol(HIP_SYMBOL(lz4m::g_cprof), z, sizeof(z));
-    }
-    return (int)e;
-#else
     (void)out;
     (void)reset;
     return -1;
-#endif
 }
 
 static thread_local int g_linked_passes = 0;

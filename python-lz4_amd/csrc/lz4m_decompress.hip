@@ -33,10 +33,7 @@
 
 namespace lz4m {
 
-#ifndef LZ4M_COOP_MIN
-#define LZ4M_COOP_MIN 64
-#endif
-constexpr int64_t kCoopMin = LZ4M_COOP_MIN;   // copies longer than this go wave-cooperative
+constexpr int64_t kCoopMin = 64;     // copies longer than this go wave-cooperative
 
 enum CopyKind : int { kNone = 0, kLiteral = 1, kMatch = 2 };
 
@@ -725,45 +722,10 @@ __device__ __forceinline__ int32_t coop_finish(const uint8_t* s, uint8_t* d, int
 // cooperative kernel: everything is flushed first and the history reloaded
 // after.  The accept/reject rules are the cooperative kernel's plus "fits in
 // the buffer", so statuses and bytes are identical.
-#ifndef LZ4M_HIST_KEEP
-#define LZ4M_HIST_KEEP 4096
-#endif
-#ifndef LZ4M_HIST_RESTAGE
-#define LZ4M_HIST_RESTAGE 384
-#endif
-#ifndef LZ4M_HIST_SWALK
-#define LZ4M_HIST_SWALK 0   // A/B: the chain of sequence starts by a serial readlane walk instead of pointer jumping (r05ai: 32 x 4 MiB 76.2 vs 43.0 ms, 16 384 x 64 KiB 9.4 vs 5.5 ms)
-#endif
 constexpr int32_t kHistW = 8192;
-constexpr int32_t kHistKeep = LZ4M_HIST_KEEP;   // history kept on a rebase (tuning macro)
+constexpr int32_t kHistKeep = 4096;      // history kept on a rebase
 constexpr int32_t kHistRebase = kHistW - 2048;
-constexpr int32_t kHistRestage = LZ4M_HIST_RESTAGE;   // restage below this many window bytes (tuning macro)
-
-// Store exactly k bytes (k >= 16: all 16) of v at LDS address p.
-__device__ __forceinline__ void lds_put_exact(lds_u8* p, u32x4 v, int32_t k) {
-    if (k >= 16) {
-        lds_st16(p, v);
-        return;
-    }
-    if (k <= 0) return;
-    uint32_t o = 0;
-    if (k & 8) {
-        const uint64_t x = ((uint64_t)v.y << 32) | v.x;
-        __builtin_memcpy((uint8_t*)p, &x, 8);
-        o = 8;
-    }
-    if (k & 4) {
-        const uint32_t x = window_dword(v, o);
-        __builtin_memcpy((uint8_t*)(p + o), &x, 4);
-        o += 4;
-    }
-    if (k & 2) {
-        const uint16_t x = (uint16_t)window_dword(v, o);
-        __builtin_memcpy((uint8_t*)(p + o), &x, 2);
-        o += 2;
-    }
-    if (k & 1) p[o] = (uint8_t)window_dword(v, o);
-}
+constexpr int32_t kHistRestage = 384;    // restage below this many window bytes
 
 __device__ __forceinline__ void lds_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
@@ -804,20 +766,6 @@ __device__ __forceinline__ bool run_len32(const uint8_t* s, int32_t& q, int32_t 
     return false;
 }
 
-// LZ4M_HIST_PROF (diagnostic builds only, tools/prof_hist.py): per-phase
-// cycle sums of hist_decompress_kernel, read with lz4m_hist_prof.
-#ifdef LZ4M_HIST_PROF
-__device__ unsigned long long g_hist_prof[16];
-#define HP_DECL uint64_t hp[16] = {0}; uint64_t hp_t = clock64();
-#define HP_MARK(i) do { const uint64_t _t = clock64(); hp[i] += _t - hp_t; hp_t = _t; } while (0)
-#define HP_COUNT(i, x) hp[i] += (uint64_t)(x)
-#define HP_FLUSH() do { if (lane == 0) for (int _i = 0; _i < 16; ++_i) atomicAdd(&g_hist_prof[_i], (unsigned long long)hp[_i]); } while (0)
-#else
-#define HP_DECL
-#define HP_MARK(i) do {} while (0)
-#define HP_COUNT(i, x) do {} while (0)
-#define HP_FLUSH() do {} while (0)
-#endif
 
 // DICT (linked frames, lz4m_decompress_batch_prefix): block b's dictionary
 // is the dict_len[b] bytes ending at d + ddelta, where d is its output slot
@@ -848,18 +796,12 @@ __device__ __forceinline__ void hist_decompress_body(const uint8_t* __restrict__
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     lds_u8* IN = (lds_u8*)ins[wv];
     lds_u8* OB = (lds_u8*)outs[wv];
-#if LZ4M_LDS_ALIGN
     __shared__ __attribute__((aligned(16))) uint32_t mtab[kPutTab];
     lds_put_table_init(mtab, threadIdx.x, 256);
     __syncthreads();
     lds_cu32* MT = (lds_cu32*)mtab;
 #define HPUT(p, v, k) lds_put_al((p), (v), (k), MT)
 #define HLD(p) lds_ld16a(p)
-#else
-#define HPUT(p, v, k) lds_put_exact((p), (v), (k))
-#define HLD(p) lds_ld16(p)
-#endif
-    HP_DECL
     const uint8_t* solo_src = nullptr;
     __shared__ int32_t solo_r, solo_lit, solo_lip;   // SOLO: result; the stored-like fast path's length and start
     uint32_t* ts = SOLO && solo_done ? reinterpret_cast<uint32_t*>(solo_done + 1) : nullptr;   // CallMeta::work
@@ -952,9 +894,7 @@ __device__ __forceinline__ void hist_decompress_body(const uint8_t* __restrict__
         const int32_t dlen = DICT ? dict_len[b] : 0;
         int32_t ip = 0, op = 0, base = 0, F = 0, ib = -kCoopIn;
         bool fit_cut = false;   // the last round stopped at a sequence that only did not fit the buffer
-        HP_MARK(15);
         while (fast) {
-            HP_COUNT(8, 1);
             if (op - base > kHistRebase || (fit_cut && op - base > kHistKeep)) {   // keep the last kHistKeep bytes
                 const int32_t nb = (op - kHistKeep) & ~15;
                 // the move distance (> 2 KiB) exceeds the 1 KiB a wave moves per pass
@@ -974,7 +914,6 @@ __device__ __forceinline__ void hist_decompress_body(const uint8_t* __restrict__
                 lds_st16(IN + 16 * lane, v);
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
             }
-            HP_MARK(0);
             // speculative parse + walk: lane k gets the k-th sequence start
             int32_t myseq = 0;
             int nseq = 0;
@@ -993,24 +932,6 @@ __device__ __forceinline__ void hist_decompress_body(const uint8_t* __restrict__
                 constexpr int32_t kNoSeq = 1023;
                 int32_t ja = qa.simple ? (int32_t)lane + qa.adv : kNoSeq;
                 int32_t jb = qb.simple ? (int32_t)lane + 64 + qb.adv : kNoSeq;
-#if LZ4M_HIST_SWALK
-                // serial walk on the scalar side: one readlane per sequence
-                {
-                    int32_t cs = 0;   // uniform: the next start, relative to pos
-                    int n2 = nseq;
-                    while (n2 < 64 && cs < 128) {
-                        const uint64_t sm = cs < 64 ? sa : sb;
-                        if (!((sm >> (cs & 63)) & 1ull)) break;   // a non-simple sequence
-                        if ((int)lane == n2) myseq = pos + cs;
-                        cs = __builtin_amdgcn_readlane(cs < 64 ? ja : jb, cs & 63);
-                        ++n2;
-                    }
-                    nseq = n2;
-                    if (nseq >= 64 || cs < 128) break;
-                    pos += cs;
-                    continue;
-                }
-#endif
                 const int32_t kk = (int32_t)lane - nseq;
                 int32_t c = kk >= 0 ? 0 : kNoSeq;
 #pragma unroll
@@ -1041,7 +962,6 @@ __device__ __forceinline__ void hist_decompress_body(const uint8_t* __restrict__
                 if (cv < 128) break;   // a non-simple sequence
                 pos += cv;
             }
-            HP_MARK(1);
             if (nseq == 0) {
                 // one sequence with literal > 12 bytes (or a long length), whole wave, on HBM
                 const uint32_t tok = s[ip];
@@ -1075,7 +995,6 @@ __device__ __forceinline__ void hist_decompress_body(const uint8_t* __restrict__
                 for (int32_t c = base + 16 * (int32_t)lane; c < op; c += 16 * kWave)
                     lds_st16(OB + (c - base), ld16(d + c));
                 F = op;
-                HP_MARK(6);
                 continue;
             }
             // sequence k in lane k
@@ -1103,8 +1022,6 @@ __device__ __forceinline__ void hist_decompress_body(const uint8_t* __restrict__
             if (use == 0 && !(fit_only && !fit_cut && op - base > kHistKeep)) break;
             fit_cut = fit_only;
             if (use == 0) continue;
-            HP_COUNT(10, use);
-            HP_MARK(2);
             const bool u = (int)lane < use;
             const int32_t m = o + lit;
             // sources older than the buffer: their first 16 bytes are requested now,
@@ -1121,7 +1038,6 @@ __device__ __forceinline__ void hist_decompress_body(const uint8_t* __restrict__
                 }
             }
             lds_wait();
-            HP_MARK(3);
             const int32_t src_end = m - off + (off < ml ? off : ml);
             // A match is ready when no pending match writes into its source: its
             // source ends before the first pending match, or the nearest pending
@@ -1159,16 +1075,13 @@ __device__ __forceinline__ void hist_decompress_body(const uint8_t* __restrict__
                 }
                 lds_wait();
                 pend &= ~__ballot(ready);
-                HP_COUNT(9, 1);
             }
-            HP_MARK(4);
             op = __builtin_amdgcn_readlane(o + len, use - 1);
             ip = ib + __builtin_amdgcn_readlane(myseq + adv, use - 1);
             // finished 16-byte chunks to HBM
             for (int32_t c = F + 16 * (int32_t)lane; c + 16 <= op; c += 16 * kWave)
                 st16(d + c, lds_ld16(OB + (c - base)));
             F += (op - F) & ~15;
-            HP_MARK(5);
             if (use < nseq && !fit_only) break;
         }
         // flush the rest exactly, then the exact state machine from (ip, op)
@@ -1181,8 +1094,6 @@ __device__ __forceinline__ void hist_decompress_body(const uint8_t* __restrict__
         if (SOLO) LZ4M_WTS(ts, 6);
         if (lane == 0) status[b] = r;
         if (SOLO && lane == 0) solo_r = r;
-        HP_MARK(7);
-        HP_COUNT(11, 1);
     }
     if constexpr (SOLO) {
         // the decoded bytes to the caller's mapped host buffer, all four waves
@@ -1235,7 +1146,6 @@ __device__ __forceinline__ void hist_decompress_body(const uint8_t* __restrict__
             if (threadIdx.x == 0) __hip_atomic_store(solo_done, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
-    HP_FLUSH();
 #undef HPUT
 #undef HLD
 }
@@ -1513,13 +1423,3 @@ extern "C" int lz4m_decompress_chain(const uint8_t* d_src, const int64_t* d_src_
     return (int)hipGetLastError();
 }
 
-#ifdef LZ4M_HIST_PROF
-extern "C" int lz4m_hist_prof(unsigned long long* out, int reset) {
-    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(lz4m::g_hist_prof), sizeof(unsigned long long) * 16);
-    if (e == hipSuccess && reset) {
-        unsigned long long z[16] = {0};
-        e = hipMemcpyToSymbol(HIP_SYMBOL(lz4m::g_hist_prof), z, sizeof(z));
-    }
-    return (int)e;
-}
-#endif

@@ -170,11 +170,8 @@ constexpr size_t kWorkIn = 66 * 1024;         // input region: the lone-block ke
 constexpr size_t kWorkOut = 1 << 20;          // output region: capacities up to 1 MiB
 constexpr size_t kWorkMb = 128;               // two mailboxes
 constexpr uint64_t kIdle = 200000;            // 2 ms of the 100 MHz real-time clock
-#ifndef LZ4M_WORKER_LIFE
-#define LZ4M_WORKER_LIFE 200000               // 2 ms of the 100 MHz clock: a launch's whole lifetime
-#endif
-constexpr uint64_t kLife = LZ4M_WORKER_LIFE;
-constexpr int32_t kSoloStageFail = LZ4M_SOLO_STAGE_FAIL;        // lone-block compress: a staging wait gave up (lz4m_compress.hip)
+constexpr uint64_t kLife = 200000;            // 2 ms: a launch's whole lifetime (r05f: 5 ms held a shared queue 5 ms)
+constexpr int32_t kSoloStageFail = LZ4M_SOLO_STAGE_FAIL;   // lone-block compress: a staging wait gave up (lz4m_compress.hip)
 
 std::atomic<int> g_worker_mode{-1};           // -1: from LZ4M_WORKER at first use
 // every call the worker path took and then handed to the launch path: a

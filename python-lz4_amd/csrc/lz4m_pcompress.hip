@@ -132,9 +132,6 @@ __device__ __forceinline__ uint32_t wave_or(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
-#ifndef LZ4M_PC_SCAT
-#define LZ4M_PC_SCAT 0   // A/B: the encoder's sequence lookup by a DPP-reduced start mask instead of a bpermute binary search (r05aj: same output, 0.3-0.7 % slower -- issue-bound, not latency-bound)
-#endif
 
 // set bits of m in lanes below this one
 __device__ __forceinline__ int32_t count_below(uint64_t m) {
@@ -188,18 +185,6 @@ __device__ __forceinline__ int32_t emit_seqs(const uint8_t* s, uint8_t* d, int32
     for (int32_t t0 = 0; t0 < ptotal; t0 += 64) {
         const int32_t t = t0 + (int32_t)lane;
         // last sequence k < ns with pbase_k <= t (pbase ascends with k)
-#if LZ4M_PC_SCAT
-        // without LDS: the sequences starting inside (t0, t0 + 64) set their
-        // bit of a wave-wide mask (OR-reduced by DPP), and lane t counts the
-        // bits at or below it on top of the last sequence starting by t0
-        const int k0 = (int)__builtin_popcountll(__ballot((int)lane < ns && pbase <= t0)) - 1;
-        const int32_t dd = pbase - t0;
-        const bool inr = (int)lane < ns && dd > 0 && dd < 64;
-        const uint32_t mlo = wave_or(inr && dd < 32 ? 1u << (dd & 31) : 0u);
-        const uint32_t mhi = wave_or(inr && dd >= 32 ? 1u << (dd & 31) : 0u);
-        const uint32_t mine = ((lane < 32 ? mlo : mhi) >> (lane & 31)) & 1u;
-        const int sq4 = (k0 + (int)__builtin_amdgcn_mbcnt_hi(mhi, __builtin_amdgcn_mbcnt_lo(mlo, 0u)) + (int)mine) << 2;
-#else
         // searched in ds_bpermute byte-address units (4 k): each step's
         // address is the previous one plus an instruction offset
         int sq4 = 0;
@@ -209,7 +194,6 @@ __device__ __forceinline__ int32_t emit_seqs(const uint8_t* s, uint8_t* d, int32
             const int32_t pk = __builtin_amdgcn_ds_bpermute(k4, pbase);
             if (k4 < 4 * ns && pk <= t) sq4 = k4;
         }
-#endif
         const int32_t pb = __builtin_amdgcn_ds_bpermute(sq4, pbase), ob = __builtin_amdgcn_ds_bpermute(sq4, obase),
                       L = __builtin_amdgcn_ds_bpermute(sq4, lit), O = __builtin_amdgcn_ds_bpermute(sq4, off),
                       M = __builtin_amdgcn_ds_bpermute(sq4, ml), S = __builtin_amdgcn_ds_bpermute(sq4, lstart);
@@ -289,9 +273,6 @@ struct Chunk {
 // candidate -- and the table ends holding each bucket's last position, as
 // with the per-hash-bit ballots it replaces.  r05n: 0.8 % slower than the
 // ballots (the 16-bit form's return needs an explicit LDS wait), so off.
-#ifndef LZ4M_PC_XCHG
-#define LZ4M_PC_XCHG 0
-#endif
 
 // WIN (blocks > 64 KiB): the table holds the low 16 bits of each position
 // (u16, as for blocks <= 64 KiB) instead of whole u32 positions, and a
@@ -304,28 +285,10 @@ template <bool BIG, int HB, bool WIN = false>
 __device__ __forceinline__ void chunk_issue(Chunk& C, const uint8_t* s, uint32_t* table32, int32_t p0, uint32_t v,
                                             int32_t N, int32_t mlast, uint32_t lane) {
     constexpr bool U32 = BIG && !WIN;   // whole positions in a u32 table
-    static_assert(!(LZ4M_PC_XCHG && WIN), "the exchange variant has no windowed table");
+    static_assert(!(0 && WIN), "the exchange variant has no windowed table");
     const int32_t p = p0 + (int32_t)lane;
     const bool act = p + 4 <= N;
     const uint32_t h = act ? phash<HB>(v) : (1u << HB);
-#if LZ4M_PC_XCHG
-    int32_t cand = -1;
-    if (act) {
-        uint32_t old;
-        if (BIG) {
-            typedef __attribute__((address_space(3))) uint32_t l32;
-            old = __hip_atomic_exchange((l32*)table32 + h, (uint32_t)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            cand = old == 0xFFFFFFFFu ? -1 : (int32_t)old;
-        } else {
-            typedef __attribute__((address_space(3))) uint16_t l16;
-            const uint32_t a = (uint32_t)(uintptr_t)((l16*)table32 + h) & ~3u, sh = (h & 1u) * 16u;
-            asm volatile("ds_mskor_rtn_b32 %0, %1, %2, %3\n\ts_waitcnt lgkmcnt(0)"
-                         : "=v"(old) : "v"(a), "v"(0xFFFFu << sh), "v"(((uint32_t)p & 0xFFFFu) << sh) : "memory");
-            old = (old >> sh) & 0xFFFFu;
-            cand = old == kEmpty ? -1 : (int32_t)old;
-        }
-    }
-#else
     // lanes with the same hash (one ballot per hash bit), hence the nearest
     // earlier one (the candidate) and whether a later one exists (then this
     // lane does not write the table)
@@ -354,7 +317,6 @@ __device__ __forceinline__ void chunk_issue(Chunk& C, const uint8_t* s, uint32_t
             table16[h] = (uint16_t)p;
         }
     }
-#endif
     C.v = v;
     C.cand = cand;
     // LZ4_DISTANCE_MAX (lz4.c:1064): only checkable past 64 KiB
@@ -389,9 +351,6 @@ __device__ __forceinline__ uint64_t chunk_finish(const Chunk& C, int32_t p0, int
     return __ballot(ok);
 }
 
-#ifndef LZ4M_PC_ORDER
-#define LZ4M_PC_ORDER 1   // 1: B's candidate loads after A's walk (r05f: +0.7-1 %); 0: before
-#endif
 // SEG (blocks > 64 KiB, lz4m_pcompress_large_batch): a block is parsed as
 // up to kSegs segments of >= 256 KiB, one wavefront each, so that a batch of
 // few large blocks (config 4: 2 048 x 4 MiB) still fills the chip.  Segment k
@@ -498,7 +457,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((BIG && !WIN
             const bool has_next = p0 + 68 <= N;
             Chunk B;
             uint32_t wafter = 0;
-            // LZ4M_PC_ORDER 1: B's loads are issued after A's walk, whose
+            // B's loads are issued after A's walk, whose
             // long-match counts and catch-up loads wait at once (gfx9 counts
             // loads in order: such a wait would also wait for B's)
             auto issue_b = [&]() __attribute__((always_inline)) {
@@ -507,7 +466,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((BIG && !WIN
                     if (p0 + 132 <= N) wafter = load_word(s, p0 + 128 + (int32_t)lane, N);
                 }
             };
-            if (!LZ4M_PC_ORDER) issue_b();
             // ---- greedy parse of chunk p0.  The serial walk only picks the
             // sequence starts: the first verified lane at or after the previous
             // match's end (catch-up moves a start back but not the end).
@@ -580,10 +538,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((BIG && !WIN
                 q_pb = __builtin_amdgcn_ds_permute(addr, ipsz - psz);
                 anchor = cur;
             }
-            if (LZ4M_PC_ORDER) issue_b();
+            issue_b();
             int32_t LB = 0, backB = 0;
             uint64_t maskB = 0;
-            if (!LZ4M_PC_ORDER && has_next) maskB = chunk_finish(B, p0 + 64, matchlimit, LB, backB, lane);
             if (ns > 0) {
                 if (SEG && f_lit < 0) {
                     f_lit = rdl(q_lit, 0);
@@ -597,7 +554,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((BIG && !WIN
                 }
                 op += w;
             }
-            if (LZ4M_PC_ORDER && has_next) maskB = chunk_finish(B, p0 + 64, matchlimit, LB, backB, lane);
+            if (has_next) maskB = chunk_finish(B, p0 + 64, matchlimit, LB, backB, lane);
             if (!has_next) break;
             vprev = A.v;
             A.v = B.v;
@@ -721,9 +678,6 @@ extern "C" size_t lz4m_pcompress_large_workspace_size(int64_t n, int32_t max_len
     return (size_t)(meta + n * segs * seg_slot(max_len > 0 ? seg_len(max_len) : kSegMin));
 }
 
-#ifndef LZ4M_PC_SEGHB
-#define LZ4M_PC_SEGHB 12   // hash bits of the segment parse
-#endif
 extern "C" int lz4m_pcompress_large_batch(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len,
                                           uint8_t* d_dst, const int64_t* d_dst_off, const int32_t* d_dst_cap,
                                           int32_t* d_out_len, int64_t n, int32_t max_len, void* d_work,
@@ -736,18 +690,11 @@ extern "C" int lz4m_pcompress_large_batch(const uint8_t* d_src, const int64_t* d
     int32_t* meta = (int32_t*)d_work;
     uint8_t* slots = (uint8_t*)d_work + ((n * segs * 16 + 255) & ~(int64_t)255);
     const int64_t cap = seg_slot(max_len > 0 ? seg_len(max_len) : kSegMin);
-    static const int hb = [] {
-        const char* e = getenv("LZ4M_PC_SEGHB");   // A/B: 12 or 13
-        return e ? atoi(e) : LZ4M_PC_SEGHB;
-    }();
     const int64_t items = n * segs;
     const uint32_t grid = (uint32_t)(items < (1ll << 30) ? items : (1ll << 30));
-    if (hb == 13)
-        hipLaunchKernelGGL((pcompress_kernel<true, 13, true, true>), dim3(grid), dim3(64), 0, st, d_src, d_src_off,
-                           d_src_len, slots, nullptr, nullptr, nullptr, n, meta, cap, segs);
-    else
-        hipLaunchKernelGGL((pcompress_kernel<true, 12, true, true>), dim3(grid), dim3(64), 0, st, d_src, d_src_off,
-                           d_src_len, slots, nullptr, nullptr, nullptr, n, meta, cap, segs);
+    // 12 hash bits (r05ba: 13 bits gained 1.9 % ratio at 1.6x the time)
+    hipLaunchKernelGGL((pcompress_kernel<true, 12, true, true>), dim3(grid), dim3(64), 0, st, d_src, d_src_off,
+                       d_src_len, slots, nullptr, nullptr, nullptr, n, meta, cap, segs);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return (int)e;
     const uint32_t sgrid = (uint32_t)(n < (1ll << 30) ? n : (1ll << 30));
@@ -757,28 +704,15 @@ extern "C" int lz4m_pcompress_large_batch(const uint8_t* d_src, const int64_t* d
 }
 
 // variant: 0 = blocks <= 64 KiB, 12-bit u16 table; 1 = the same with 13 bits;
-// 2 = any block size: a 13-bit u32 table, or (LZ4M_PC_LARGE) a windowed u16 table
-#ifndef LZ4M_PC_LARGE_DEFAULT
-#define LZ4M_PC_LARGE_DEFAULT 13   // r05ay: 303 -> 167 ms on config 4, same size
-#endif
+// 2 = any block size: a windowed 13-bit u16 table (r05ay: 303 -> 167 ms on
+// config 4 against a u32 table, same size)
 int pcompress_launch(const uint8_t* d_src, const int64_t* d_src_off, const int32_t* d_src_len, uint8_t* d_dst,
                      const int64_t* d_dst_off, const int32_t* d_dst_cap, int32_t* d_out_len, int64_t n, int variant,
                      hipStream_t stream) {
     const uint32_t grid = (uint32_t)(n < (1ll << 30) ? n : (1ll << 30));
     if (variant == 2) {
-        static const int large = [] {   // LZ4M_PC_LARGE (A/B): 0 = u32 table, 12 / 13 = windowed u16 table of that many bits
-            const char* e = getenv("LZ4M_PC_LARGE");
-            return e ? atoi(e) : LZ4M_PC_LARGE_DEFAULT;
-        }();
-        if (large == 12)
-            hipLaunchKernelGGL((pcompress_kernel<true, 12, true>), dim3(grid), dim3(64), 0, stream, d_src, d_src_off,
-                               d_src_len, d_dst, d_dst_off, d_dst_cap, d_out_len, n);
-        else if (large == 13)
-            hipLaunchKernelGGL((pcompress_kernel<true, 13, true>), dim3(grid), dim3(64), 0, stream, d_src, d_src_off,
-                               d_src_len, d_dst, d_dst_off, d_dst_cap, d_out_len, n);
-        else
-            hipLaunchKernelGGL((pcompress_kernel<true, 13>), dim3(grid), dim3(64), 0, stream, d_src, d_src_off,
-                               d_src_len, d_dst, d_dst_off, d_dst_cap, d_out_len, n);
+        hipLaunchKernelGGL((pcompress_kernel<true, 13, true>), dim3(grid), dim3(64), 0, stream, d_src, d_src_off,
+                           d_src_len, d_dst, d_dst_off, d_dst_cap, d_out_len, n);
     } else if (variant == 1) {
         hipLaunchKernelGGL((pcompress_kernel<false, 13>), dim3(grid), dim3(64), 0, stream, d_src, d_src_off,
                            d_src_len, d_dst, d_dst_off, d_dst_cap, d_out_len, n);

@@ -18,12 +18,9 @@ struct RowMeta {
 };
 static_assert(sizeof(RowMeta) == 32, "RowMeta layout");
 
-// scratch layout: 64 bytes of counters, 256 KiB of dummy targets (the
-// unconditional flush stores of lanes with nothing final: 1 KiB per wave
-// slot, blockIdx % 256), one RowMeta per block, then the length bytes
-constexpr size_t kRowsDummy = 64;
-constexpr size_t kRowsDummySlots = 256;
-constexpr size_t kRowsMeta = kRowsDummy + kRowsDummySlots * 1024;
+// scratch layout: 64 bytes of counters, one RowMeta per block, then the
+// length bytes
+constexpr size_t kRowsMeta = 64;
 
 }  // namespace lz4m
 

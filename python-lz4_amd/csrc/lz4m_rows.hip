@@ -37,21 +37,6 @@
 namespace lz4m {
 typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
 
-// LZ4M_ROWS_PROF (diagnostic builds only, tools/prof_rows.sh): per-phase
-// wave-cycle sums and event counts of the two kernels, read with lz4m_rows_prof.
-#ifdef LZ4M_ROWS_PROF
-__device__ unsigned long long g_rows_prof[32];
-#define RP_DECL uint64_t rp[32] = {0}; uint64_t rp_t = clock64();
-#define RP_MARK(i) do { const uint64_t _t = clock64(); rp[i] += _t - rp_t; rp_t = _t; } while (0)
-#define RP_COUNT(i, x) rp[i] += (uint64_t)(x)
-#define RP_FLUSH(a, b) do { if (lane == 0) for (int _i = (a); _i < (b); ++_i) atomicAdd(&g_rows_prof[_i], (unsigned long long)rp[_i]); } while (0)
-#else
-#define RP_DECL
-#define RP_MARK(i) do {} while (0)
-#define RP_COUNT(i, x) do {} while (0)
-#define RP_FLUSH(a, b) do {} while (0)
-#endif
-
 // s_waitcnt vmcnt(0) (expcnt and lgkmcnt left at their maximum)
 __device__ __forceinline__ void wait_vm0() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 
@@ -103,107 +88,6 @@ __device__ __forceinline__ void row_excl_max2(int32_t a, int32_t b, int32_t& xa,
     y = max(y, __builtin_amdgcn_update_dpp(0, y, 0x118, 0xF, 0xF, false));
     xa = x;
     xb = y;
-}
-
-// LDS accesses at arbitrary byte offsets of a history buffer.  A _b64 /
-// _b128 DS access off its natural alignment is replayed (MI355X: ~64 cycles
-// per wave-instruction, cdna_hip_programming.md Guideline 17), so
-// LZ4M_LDS_NARROW builds these from 4-byte and narrower accesses.
-#ifndef LZ4M_LDS_NARROW
-#define LZ4M_LDS_NARROW 0
-#endif
-// (volatile: the load/store vectoriser would merge neighbouring 4-byte
-// accesses back into one unaligned wide one)
-typedef __attribute__((address_space(3))) volatile uint32_t lds_vu32 __attribute__((aligned(1)));
-__device__ __forceinline__ uint32_t lds_ld4(const lds_u8* p) { return *(const lds_vu32*)p; }
-__device__ __forceinline__ void lds_st4(lds_u8* p, uint32_t x) { *(lds_vu32*)p = x; }
-__device__ __forceinline__ void lds_st8(lds_u8* p, uint32_t lo, uint32_t hi) {
-#if LZ4M_LDS_NARROW
-    lds_st4(p, lo);
-    lds_st4(p + 4, hi);
-#else
-    const uint64_t x = ((uint64_t)hi << 32) | lo;
-    __builtin_memcpy((uint8_t*)p, &x, 8);
-#endif
-}
-// 16 bytes at any byte offset
-__device__ __forceinline__ u32x4 lds_ld16a(const lds_u8* p);
-__device__ __forceinline__ u32x4 lds_ld16u(const lds_u8* p) {
-#if LZ4M_LDS_ALIGN
-    return lds_ld16a(p);
-#elif LZ4M_LDS_NARROW
-    return u32x4{lds_ld4(p), lds_ld4(p + 4), lds_ld4(p + 8), lds_ld4(p + 12)};
-#else
-    return lds_ld16(p);
-#endif
-}
-__device__ __forceinline__ void lds_st16u(lds_u8* p, u32x4 v) {
-#if LZ4M_LDS_NARROW
-    lds_st4(p, v.x);
-    lds_st4(p + 4, v.y);
-    lds_st4(p + 8, v.z);
-    lds_st4(p + 12, v.w);
-#else
-    lds_st16(p, v);
-#endif
-}
-
-// Exactly k bytes (k >= 16: 16; k <= 0: none) of v at LDS address p.
-__device__ __forceinline__ void lds_put(lds_u8* p, u32x4 v, int32_t k) {
-    if (k >= 16) {
-        lds_st16u(p, v);
-        return;
-    }
-    if (k <= 0) return;
-    uint32_t o = 0;
-    if (k & 8) {
-        lds_st8(p, v.x, v.y);
-        o = 8;
-    }
-    if (k & 4) {
-        const uint32_t x = window_dword(v, o);
-        __builtin_memcpy((uint8_t*)(p + o), &x, 4);
-        o += 4;
-    }
-    if (k & 2) {
-        const uint16_t x = (uint16_t)window_dword(v, o);
-        __builtin_memcpy((uint8_t*)(p + o), &x, 2);
-        o += 2;
-    }
-    if (k & 1) p[o] = (uint8_t)window_dword(v, o);
-}
-
-// Exactly k bytes (k >= 16: 16; k <= 0: none) of v at LDS address p,
-// without branches: the pieces that are not needed are written to the lane's
-// private 16-byte slot `dummy` instead (five LDS writes, ~15 VALU).
-__device__ __forceinline__ void lds_put_bf(lds_u8* p, lds_u8* dummy, u32x4 v, int32_t k) {
-    const bool full = k >= 16;
-    const uint32_t km = full ? 0u : (uint32_t)(k > 0 ? k : 0);
-    const bool b8 = (km & 8) != 0, b4 = (km & 4) != 0, b2 = (km & 2) != 0, b1 = (km & 1) != 0;
-    if (__any(full)) lds_st16u(full ? p : dummy, v);   // 16-byte pieces are the rarer case
-    lds_st8(b8 ? p : dummy, v.x, v.y);
-    const uint32_t d4 = b8 ? v.z : v.x;                       // dword at offset km & 8
-    __builtin_memcpy((uint8_t*)(b4 ? p + (km & 8) : dummy), &d4, 4);
-    const uint32_t d2 = b4 ? (b8 ? v.w : v.y) : d4;           // dword at offset km & 12
-    const uint16_t h2 = (uint16_t)d2;
-    __builtin_memcpy((uint8_t*)(b2 ? p + (km & 12) : dummy), &h2, 2);
-    *(b1 ? p + (km & 14) : dummy) = (uint8_t)(b2 ? (d2 >> 16) : d2);
-}
-
-// Exactly k (1..) bytes (k >= 16: 16) of v at LDS address p: each piece
-// written by the lanes that need it only (an LDS access costs per active
-// lane), with no branches around the pieces.
-__device__ __forceinline__ void lds_put_masked(lds_u8* p, u32x4 v, int32_t k) {
-    const bool full = k >= 16;
-    const uint32_t km = full ? 0u : (uint32_t)k;
-    if (full) lds_st16u(p, v);
-    if (km & 8) lds_st8(p, v.x, v.y);
-    const uint32_t d4 = (km & 8) ? v.z : v.x;
-    if (km & 4) __builtin_memcpy((uint8_t*)(p + (km & 8)), &d4, 4);
-    const uint32_t d2 = (km & 4) ? ((km & 8) ? v.w : v.y) : d4;
-    const uint16_t h2 = (uint16_t)d2;
-    if (km & 2) __builtin_memcpy((uint8_t*)(p + (km & 12)), &h2, 2);
-    if (km & 1) *(p + (km & 14)) = (uint8_t)((km & 2) ? (d2 >> 16) : d2);
 }
 
 // Exactly k bytes (k >= 16: 16) of v at global address p.
@@ -266,7 +150,7 @@ __device__ __forceinline__ uint32_t dword32(u32x4 a, u32x4 b, uint32_t k) {
 // ------------------------------------------------------------ 1. the parse
 // One lane per block.  The compressed block is read through a 128-byte LDS
 // ring per lane holding stream bytes [wb, wb + 128) (wb a multiple of 64; a
-// 16-byte mirror after the ring keeps every 16-byte read contiguous), and the
+// 16-byte read wraps per aligned 8-byte piece), and the
 // next 64 bytes [wb + 128, wb + 192) are requested ahead into registers.  The
 // inner loop is the common sequence only -- literal <= 12 bytes, at most one
 // match-length byte, inside the ring, good -- as straight-line code (one
@@ -275,16 +159,12 @@ __device__ __forceinline__ uint32_t dword32(u32x4 a, u32x4 b, uint32_t k) {
 // waits; once too few lanes can go on, the wave runs one general step: every
 // lane past the first half of its ring rotates the requested bytes in and
 // requests the next 64, waiting lanes parse one sequence with the general
-// parse.  Recorded lengths are staged in a 64-entry LDS ring per lane and
-// leave for HBM 32 at a time.
+// parse.  Recorded lengths are staged in a 32-entry LDS ring per lane and
+// leave for HBM 16 at a time.  The ring refills are loaded by four lanes per
+// block (one 64-byte request instead of four 16-byte ones).
 constexpr int kPW = 128;                // ring bytes
-#ifndef LZ4M_PARSE_NOMIRROR
-#define LZ4M_PARSE_NOMIRROR 1           // 16-byte ring reads wrap per aligned 8-byte piece (no mirror: 16 waves/CU, -0.9 ms)
-#endif
-constexpr int kPWS = LZ4M_PARSE_NOMIRROR ? kPW : kPW + 16;   // ring (+ mirror)
 // 16 ring bytes at ring offset x (0..kPW-1)
 __device__ __forceinline__ u32x4 ring_ld16(const lds_u8* W, int32_t x) {
-#if LZ4M_PARSE_NOMIRROR
     // three aligned 8-byte reads, each wrapped into the ring, and a funnel shift
     const uint32_t a = (uint32_t)x & ~7u;
     const uint64_t x0 = *(const lds_vu64*)(W + a), x1 = *(const lds_vu64*)(W + ((a + 8u) & (kPW - 1))),
@@ -296,43 +176,21 @@ __device__ __forceinline__ u32x4 ring_ld16(const lds_u8* W, int32_t x) {
     const uint32_t e0 = h ? c1 : c0, e1 = h ? c2 : c1, e2 = h ? c3 : c2, e3 = h ? c4 : c3, e4 = h ? c5 : c4;
     return u32x4{__builtin_amdgcn_alignbyte(e1, e0, r), __builtin_amdgcn_alignbyte(e2, e1, r),
                  __builtin_amdgcn_alignbyte(e3, e2, r), __builtin_amdgcn_alignbyte(e4, e3, r)};
-#else
-    return lds_ld16u(W + x);
-#endif
 }
-#ifndef LZ4M_PARSE_STAGE
-#define LZ4M_PARSE_STAGE 32
-#endif
-constexpr int kPStage = LZ4M_PARSE_STAGE;   // length ring (flushed in halves)
-static_assert(kPStage == 32 || kPStage == 64, "length ring: 32 or 64 entries");
-#ifndef LZ4M_PARSE_WG
-#define LZ4M_PARSE_WG 64
-#endif
-constexpr int kPWG = LZ4M_PARSE_WG;     // parse workgroup (LDS is allocated per workgroup)
-#ifndef LZ4M_PARSE_COOP
-#define LZ4M_PARSE_COOP 1               // A/B: ring refills loaded by four lanes per block (64-byte requests)
-#endif
+constexpr int kPStage = 32;   // length ring (flushed in halves)
+constexpr int kPWG = 64;      // parse workgroup (LDS is allocated per workgroup)
 // a 64-bit address received from another lane, as a global pointer
 __device__ __forceinline__ const uint8_t* readlane_safe_ptr(uint64_t a) {
     typedef __attribute__((address_space(1))) const uint8_t gu8;
     return (const uint8_t*)(gu8*)(uintptr_t)a;
 }
-#ifndef LZ4M_PARSE_V2
-#define LZ4M_PARSE_V2 1                 // predicated two-step fast loop; ring / length-ring stops skip the general parse; one-extension-byte general parse
-#endif
-#ifndef LZ4M_PARSE_RUNCAP
-#define LZ4M_PARSE_RUNCAP 16            // length-byte runs longer than this end the good prefix (finisher)
-#endif
-constexpr int32_t kPRunCap = LZ4M_PARSE_RUNCAP;
-#ifndef LZ4M_PARSE_MIN_ACTIVE
-#define LZ4M_PARSE_MIN_ACTIVE 40        // run the general step once fewer lanes than this can go on
-#endif
+constexpr int32_t kPRunCap = 16;        // length-byte runs longer than this end the good prefix (finisher)
+constexpr int kPMinActive = 40;         // run the general step once fewer lanes than this can go on
 
-// 64 stream bytes into ring half h (0: offsets 0-63, with the mirror; 1: 64-127)
+// 64 stream bytes into ring half h (0: offsets 0-63; 1: 64-127)
 __device__ __forceinline__ void ring_put(lds_u8* W, int32_t h, const u32x4* v) {
 #pragma unroll
     for (int c = 0; c < 4; ++c) lds_st16(W + 64 * h + 16 * c, v[c]);
-    if (!LZ4M_PARSE_NOMIRROR && h == 0) lds_st16(W + kPW, v[0]);
 }
 
 __device__ __forceinline__ void load64(const uint8_t* s, int32_t x, int32_t iend, u32x4* v) {
@@ -349,19 +207,17 @@ __global__ __launch_bounds__(kPWG) void rows_parse_kernel(const uint8_t* __restr
                                                          const int32_t* __restrict__ dst_cap, int64_t n,
                                                          RowMeta* __restrict__ meta, uint8_t* __restrict__ lens,
                                                          int64_t lens_cap, unsigned long long* __restrict__ ctr) {
-    __shared__ __attribute__((aligned(16))) uint8_t wins[kPWG * kPWS];
+    __shared__ __attribute__((aligned(16))) uint8_t wins[kPWG * kPW];
     __shared__ __attribute__((aligned(16))) uint8_t stgs[kPWG * kPStage];
     const uint32_t lane = lane_id();
-    lds_u8* W = (lds_u8*)(wins + threadIdx.x * kPWS);
+    lds_u8* W = (lds_u8*)(wins + threadIdx.x * kPW);
     lds_u8* stg = (lds_u8*)(stgs + threadIdx.x * kPStage);
     const uint8_t* s = nullptr;
     int64_t idx = -1, loff = 0;
     int32_t iend = 0, oend = 0, ip = 0, op = 0, k = 0, kf = 0, wb = 0;
     u32x4 pf[4];   // stream bytes [wb + 128, wb + 192), requested ahead
     bool live = false, need = false, more = true, pfv = false, stall = false;
-    RP_DECL
     while (true) {
-        RP_MARK(2);
         if (more) {
             // idle lanes take the next blocks: one queue atomic and one
             // length-space atomic per wave refill
@@ -418,16 +274,12 @@ __global__ __launch_bounds__(kPWG) void rows_parse_kernel(const uint8_t* __restr
                 }
             }
         }
-        RP_MARK(0);
         if (!__any(live)) {
             if (more) continue;
             break;
         }
-        RP_COUNT(4, 1);
-        RP_COUNT(6, __popcll(__ballot(live && need)));
         // ---- the general step
         // rotate requested bytes in (every lane past the first half of its ring)
-#if LZ4M_PARSE_COOP
         {
             // block b's 64 requested bytes are held by lanes 4 (b % 16) ..
             // + 3, 16 bytes each, in pf[b / 16]
@@ -438,10 +290,9 @@ __global__ __launch_bounds__(kPWG) void rows_parse_kernel(const uint8_t* __restr
                     const int bb = 16 * c + (int)(lane >> 2);
                     const int32_t wbb = __builtin_amdgcn_ds_bpermute(bb << 2, wb);
                     if ((R >> bb) & 1ull) {
-                        lds_u8* Wb = (lds_u8*)(wins + bb * kPWS);
+                        lds_u8* Wb = (lds_u8*)(wins + bb * kPW);
                         const int32_t h = (wbb >> 6) & 1;
                         lds_st16(Wb + 64 * h + 16 * (int32_t)(lane & 3), pf[c]);
-                        if (!LZ4M_PARSE_NOMIRROR && h == 0 && (lane & 3) == 0) lds_st16(Wb + kPW, pf[c]);
                     }
                 }
                 if ((R >> lane) & 1ull) {
@@ -450,20 +301,11 @@ __global__ __launch_bounds__(kPWG) void rows_parse_kernel(const uint8_t* __restr
                 }
             }
         }
-#else
-        if (live && pfv && ip >= wb + 64) {
-            ring_put(W, (wb >> 6) & 1, pf);
-            wb += 64;
-            pfv = false;
-        }
-#endif
-#if LZ4M_PARSE_V2
         // a lane stopped at its ring's end that the rotation could not serve
         // (nothing requested: the ring already ends at the input's end) takes
         // the general parse; every other stopped lane retries the fast loop
         if (live && stall && !need && ip + 16 > wb + kPW) need = true;
         stall = false;
-#endif
         if (live && need) {
             need = false;
             if (ip + 32 > wb + kPW) {   // no bytes ahead (block start, a long literal): load the ring now
@@ -481,7 +323,6 @@ __global__ __launch_bounds__(kPWG) void rows_parse_kernel(const uint8_t* __restr
             bool good = true, slow = true;
             int32_t pe = 0;
             int64_t lit = 0, ml = 0;
-#if LZ4M_PARSE_V2
             // straight-line from the 32 ring bytes at ip (the ring holds them:
             // loaded above if not): literal and match lengths with at most one
             // extension byte each, offset inside the 32 bytes -- the same
@@ -536,8 +377,7 @@ __global__ __launch_bounds__(kPWG) void rows_parse_kernel(const uint8_t* __restr
                     ml = M;
                 }
             }
-#endif
-            if (slow) {   // (LZ4M_PARSE_V2: rare) byte by byte; bytes outside the ring come from HBM
+            if (slow) {   // (rare) byte by byte; bytes outside the ring come from HBM
 #define PB(x) ((x) - wb < kPW ? (uint32_t)W[(x) & (kPW - 1)] : (uint32_t)s[(x)])
                 good = true;
                 const uint32_t tok = PB(ip);
@@ -604,11 +444,9 @@ __global__ __launch_bounds__(kPWG) void rows_parse_kernel(const uint8_t* __restr
         if (live && k - kf >= kPStage / 2) {
             uint8_t* o = lens + loff + kf;
             st16(o, lds_ld16(stg + (kf & (kPStage - 1))));
-            if (kPStage == 64) st16(o + 16, lds_ld16(stg + (kf & (kPStage - 1)) + 16));
             kf += kPStage / 2;
         }
         // request the next 64 bytes ahead
-#if LZ4M_PARSE_COOP
         {
             // four lanes per block, 16 contiguous bytes each: one 64-byte
             // request per block instead of four 16-byte ones
@@ -630,16 +468,8 @@ __global__ __launch_bounds__(kPWG) void rows_parse_kernel(const uint8_t* __restr
                 if ((Q >> lane) & 1ull) pfv = true;
             }
         }
-#else
-        if (live && !pfv && wb + kPW < iend) {
-            load64(s, wb + kPW, iend, pf);
-            pfv = true;
-        }
-#endif
         // ---- the common sequence, straight-line, until too few lanes can go on
-        RP_MARK(1);
-        const int32_t thr = min(LZ4M_PARSE_MIN_ACTIVE, (int)__popcll(__ballot(live)));
-#if LZ4M_PARSE_V2
+        const int32_t thr = min(kPMinActive, (int)__popcll(__ballot(live)));
         // two steps per count of the lanes that can go on; every lane runs
         // both (predicated, no exec-mask branches): a lane that cannot take
         // its sequence stops (`stall`) -- at its ring's end or a full length
@@ -649,8 +479,6 @@ __global__ __launch_bounds__(kPWG) void rows_parse_kernel(const uint8_t* __restr
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
                 const bool go = live && !need && !stall;
-                RP_COUNT(3, u == 0);
-                RP_COUNT(5, u == 0 ? __popcll(__ballot(go)) : 0);
                 const bool inw = ip + 16 <= wb + kPW;
                 const bool room = k - kf < kPStage - 1;
                 const u32x4 w = ring_ld16(W, ip & (kPW - 1));
@@ -676,38 +504,7 @@ __global__ __launch_bounds__(kPWG) void rows_parse_kernel(const uint8_t* __restr
             }
             if ((int)__popcll(__ballot(live && !need && !stall)) < max(thr, 1)) break;
         }
-#else
-        while (true) {
-            const bool go = live && !need;
-            if ((int)__popcll(__ballot(go)) < max(thr, 1)) break;
-            RP_COUNT(3, 1);
-            RP_COUNT(5, __popcll(__ballot(go)));
-            if (go) {
-                // straight-line: no short-circuit tests
-                const bool inw = ip + 16 <= wb + kPW;
-                const u32x4 w = ring_ld16(W, ip & (kPW - 1));
-                const int32_t tok = (int32_t)(w.x & 0xFFu), lit = tok >> 4, mlc = tok & 15;
-                const bool mlx = mlc == 15;
-                const uint32_t dw = dword_at(w, (uint32_t)(1 + lit));   // offset, then the match-length byte
-                const int32_t off = (int32_t)(dw & 0xFFFFu);
-                const int32_t ext = (int32_t)((dw >> 16) & 0xFFu);
-                const int32_t adv = 3 + lit + (int32_t)mlx;
-                const int32_t ml = mlc + 4 + (mlx ? ext : 0);
-                const bool ok = inw & (lit <= 12) & !(mlx & (ext == 255)) & (ip + 1 <= iend - 17) &
-                                (!mlx | (ip + adv <= iend - 4)) & (off != 0) & (off <= op + lit) &
-                                (op + lit + ml < oend - 64) & (k - kf < kPStage - 1);
-                // slot k is free (one slot of the ring always is): written even
-                // when the sequence is not taken, then overwritten
-                stg[k & (kPStage - 1)] = (uint8_t)adv;
-                ip += ok ? adv : 0;
-                op += ok ? lit + ml : 0;
-                k += (int32_t)ok;
-                need = !ok;
-            }
-        }
-#endif
     }
-    RP_FLUSH(0, 8);
 }
 
 // ------------------------------------------------------- 2. row execution
@@ -716,29 +513,7 @@ __global__ __launch_bounds__(kPWG) void rows_parse_kernel(const uint8_t* __restr
 // the row knows from the recorded lengths (row prefix sum).  The lengths and
 // the 32 bytes of the NEXT round are requested while this round copies, so a
 // round waits on at most one memory round trip (its far match sources).
-#ifndef LZ4M_ROWS_H
-#define LZ4M_ROWS_H 1024   // history per row (bytes): 1 KiB measured as fast as 2 KiB at equal occupancy
-#endif
-constexpr int32_t kRowsH = LZ4M_ROWS_H;
-#ifndef LZ4M_ROWS_LITPUT
-#define LZ4M_ROWS_LITPUT 0   // A/B: 1 = literal put only for lanes with a literal, 2 = and per piece
-#endif
-#ifndef LZ4M_ROWS_PUTMASK
-#define LZ4M_ROWS_PUTMASK 3   // 0 = branch-free dummy-slot puts (round 2); 1 = pass puts exec-masked; 2 = literal puts too; 3 = the whole pass body masked to the ready lanes
-#endif
-#ifndef LZ4M_ROWS_PASS1
-#define LZ4M_ROWS_PASS1 0     // A/B: a first readiness pass without the row scans (sources before the round)
-#endif
-#ifndef LZ4M_ROWS_ORDER
-#define LZ4M_ROWS_ORDER 1   // 1 (required: FarSrc is shared by P and Q): parse ahead after this round's passes
-#endif
-static_assert(LZ4M_ROWS_ORDER == 1, "the far-source pieces (FarSrc) are reused by the round parsed ahead");
-#ifndef LZ4M_ROWS_FARXS
-#define LZ4M_ROWS_FARXS 0   // far sources read back from the lane's literal slot (A/B)
-#endif
-#ifndef LZ4M_ROWS_OFFTREE
-#define LZ4M_ROWS_OFFTREE 1   // the offset's dword pair by a select tree (r05v A/B)
-#endif
+constexpr int32_t kRowsH = 1024;   // history per row (bytes): 1 KiB measured as fast as 2 KiB at equal occupancy
 #ifndef LZ4M_ROWS_OFFLDS
 // 1: the match offset read back from the literal's LDS slot (72 VALU fewer
 // in the kernel).  r05q: the first rows test ended in an illegal memory
@@ -746,26 +521,9 @@ static_assert(LZ4M_ROWS_ORDER == 1, "the far-source pieces (FarSrc) are reused b
 // form's), so it stays off and is not run again until it is
 #define LZ4M_ROWS_OFFLDS 0
 #endif
-#ifndef LZ4M_ROWS_ENDS
-#define LZ4M_ROWS_ENDS 1    // a round whose rows all take 16 sequences: next (ip, op) = lane 15's ends (no scans)
-#endif
-#ifndef LZ4M_ROWS_XP
-#define LZ4M_ROWS_XP 0      // timing probes, WRONG output (r05a): 2 no HBM loads in passes, 4 no late loads, 8 no far prefetch,
-                            // (r05i) 16 one pass without scans, 32 no literal puts, 64 no flush stores, 128 no match copies, 256 no rebase copy,
-                            // (r05j) 512 no long-match loop, 1024 no match puts, 2048 no match-source LDS reads
-#endif
-#ifndef LZ4M_ROWS_COUNTED
-#define LZ4M_ROWS_COUNTED 0   // A/B: a fixed number of memory operations per round on the common path (measured -1 %)
-#endif
 constexpr int32_t kRowsHS = kRowsH + 32;   // buffer stride (16-byte reads past the end stay inside)
-#ifndef LZ4M_ROWS_KEEP
-#define LZ4M_ROWS_KEEP (kRowsH / 2)
-#endif
-#ifndef LZ4M_ROWS_ROOM
-#define LZ4M_ROWS_ROOM 512
-#endif
-constexpr int32_t kRowsKeep = LZ4M_ROWS_KEEP;   // history kept on a rebase
-constexpr int32_t kRowsRoom = LZ4M_ROWS_ROOM;   // rebase when less room than this is left
+constexpr int32_t kRowsKeep = kRowsH / 2;   // history kept on a rebase
+constexpr int32_t kRowsRoom = 512;          // rebase when less room than this is left
 static_assert(kRowsKeep % 16 == 0 && kRowsKeep + kRowsRoom <= kRowsH, "history split");
 
 // Row-cooperative exact copies in HBM (16 lanes, lane j = jj).
@@ -860,7 +618,7 @@ __device__ __forceinline__ void parse_round(PSeq& P, int32_t jj, int32_t r, int3
     // (lit > 29: the offset lies past the 32 bytes, `slow` re-reads it: any
     // shift in 0..31 will do -- a wider one would be undefined)
     const uint32_t bsh = lit > 28 ? 8u : 0u;
-#elif LZ4M_ROWS_OFFTREE
+#else
     // the dword pair at pq selected by a tree on its three index bits (14
     // selects) for every lane, instead of a 16-byte and a 32-byte select chain
     // both computed and selected between
@@ -869,10 +627,6 @@ __device__ __forceinline__ void parse_round(PSeq& P, int32_t jj, int32_t r, int3
     // (po > 29: past the 32 bytes, `slow` re-reads the offset: any shift in
     // 0..31 will do -- 8 * (po - pq) would reach 32 and be undefined)
     const uint32_t bsh = po > 28 ? 8u : 0u;
-#else
-    const uint32_t pq = (uint32_t)(po < 28 ? po : 28);
-    const uint32_t dwo = lit <= 12 ? window_dword(wa, (uint32_t)po) : dword32(wa, wb, pq);
-    const uint32_t bsh = 8u * ((uint32_t)po - pq);
 #endif
     int32_t off = (int32_t)((dwo >> bsh) & 0xFFFFu);
     const int32_t e0 = (int32_t)((dwo >> (bsh + 16)) & 0xFFu);
@@ -891,9 +645,6 @@ __device__ __forceinline__ void parse_round(PSeq& P, int32_t jj, int32_t r, int3
                 ml += (int32_t)b;
             } while (b == 255 && pe < iend - t);
         }
-#if LZ4M_ROWS_COUNTED
-        wait_vm0();   // rare: so that no later use of off / ml waits on every path
-#endif
     }
     ml += 4;
     const int32_t len = act && !esc ? lit + ml : 0;
@@ -904,7 +655,7 @@ __device__ __forceinline__ void parse_round(PSeq& P, int32_t jj, int32_t r, int3
     const uint32_t rb = (uint32_t)(nok >> (16 * r)) & 0xFFFFu;
     const int32_t use = rb ? __builtin_ctz(rb) : 16;
     const bool u = jj < use;
-    if (LZ4M_ROWS_ENDS && nok == 0) {   // every row takes its 16 sequences: the ends of lane 15's
+    if (nok == 0) {   // every row takes its 16 sequences: the ends of lane 15's
         P.opn = row_last(o + len);
         P.ipn = row_last(t + dlt);
     } else {
@@ -916,13 +667,9 @@ __device__ __forceinline__ void parse_round(PSeq& P, int32_t jj, int32_t r, int3
     const bool late = far & (s0 + 32 > F);
     const bool pf = far & !late;
     // unconditional requests (lanes without a far source read the block start)
-    if (LZ4M_ROWS_XP & 8) {
-        FS.g0 = FS.g1 = u32x4{(uint32_t)s0, 0, 0, 0};
-    } else {
-        FS.g0 = ld16(d + (pf ? s0 : 0));
-        // the second piece [s0 + 16, s0 + 32) is flushed too (not late: s0 + 32 <= F)
-        FS.g1 = ld16(d + ((pf & (ml > 16)) ? s0 + 16 : 0));
-    }
+    FS.g0 = ld16(d + (pf ? s0 : 0));
+    // the second piece [s0 + 16, s0 + 32) is flushed too (not late: s0 + 32 <= F)
+    FS.g1 = ld16(d + ((pf & (ml > 16)) ? s0 + 16 : 0));
 #if !LZ4M_ROWS_OFFLDS
     const uint32_t sh = (uint32_t)lp;
     XS[0] = u32x4{__builtin_amdgcn_alignbyte(wa.y, wa.x, sh), __builtin_amdgcn_alignbyte(wa.z, wa.y, sh),
@@ -953,62 +700,31 @@ __device__ __forceinline__ int32_t next_base(int32_t op, int32_t base) {
     return op - base > kRowsH - kRowsRoom ? ((op - kRowsKeep) & ~15) : base;
 }
 
-// LZ4M_ROWS_NT: the compressed input and the length bytes are streamed (each
-// line read by one row, in order) -- non-temporal loads, so that they do not
-// push the blocks' recently flushed output (the far match sources) out of L2
-#ifndef LZ4M_ROWS_NT
-#define LZ4M_ROWS_NT 0
-#endif
-typedef u32x4 u32x4_u __attribute__((aligned(1)));
-__device__ __forceinline__ u32x4 ld16s(const uint8_t* p) {
-#if LZ4M_ROWS_NT
-    return __builtin_nontemporal_load((const u32x4_u*)p);
-#else
-    return ld16(p);
-#endif
-}
 // the round's inputs: 32 bytes at t (clamped into the block) and a length byte
 __device__ __forceinline__ void load_in(const uint8_t* s, int32_t t, int32_t iend, u32x4& a, u32x4& b) {
     const int32_t ta = t + 16 <= iend ? t : 0;   // good sequences: t + 16 < iend
     const int32_t tb = t + 32 <= iend ? t + 16 : iend - 16;
-    a = ld16s(s + ta);
-    b = ld16s(s + tb);
+    a = ld16(s + ta);
+    b = ld16(s + tb);
 }
 // (no select on the loaded value: a lane past the block's good sequences
 // reads the last length, and parse_round masks it by `act`; a select here
 // waited for the load at once)
 __device__ __forceinline__ int32_t load_len(const uint8_t* dl, int32_t k, int32_t nseq) {
-#if LZ4M_ROWS_NT
-    return (int32_t)__builtin_nontemporal_load(dl + (k < nseq ? k : nseq - 1));
-#else
     return (int32_t)dl[k < nseq ? k : nseq - 1];
-#endif
 }
 
-#if LZ4M_LDS_ALIGN
 #define LDS_PUT(p, v, k) lds_put_al((p), (v), (k), MT)
-#else
-#define LDS_PUT(p, v, k) lds_put((p), (v), (k))
-#endif
-#if LZ4M_LDS_ALIGN && LZ4M_ROWS_PUTMASK < 3
-#error "LZ4M_LDS_ALIGN needs LZ4M_ROWS_PUTMASK >= 3"
-#endif
 
 // Rows in flight: round R executes while round R + 1 is already parsed
 // (its far sources in flight) and round R + 2's inputs are requested, so a
-// round waits on no memory latency of its own.
-#ifndef LZ4M_ROWS_WAVES
-#define LZ4M_ROWS_WAVES 5   // waves per SIMD the executor's registers are held to (LDS allows 5)
-#endif
-// LZ4M_ROWS_EWG: threads per workgroup (64 or 256).  The waves of a
-// workgroup are independent (no barrier after the prologue); 256 shares the
-// put-mask and period tables (1.6 KB of LDS) between four waves.
-#ifndef LZ4M_ROWS_EWG
-#define LZ4M_ROWS_EWG 256
-#endif
-constexpr int kEWG = LZ4M_ROWS_EWG;
-static_assert(kEWG == 64 || kEWG == 256, "executor workgroup: 64 or 256 threads");
-__global__ __launch_bounds__(kEWG) __attribute__((amdgpu_waves_per_eu(LZ4M_ROWS_WAVES, 8))) void rows_exec_kernel(const uint8_t* __restrict__ src,
+// round waits on no memory latency of its own.  The registers are held to 5
+// waves per SIMD (the LDS allows 5; 6 spilled, r05bg).
+// kEWG: threads per workgroup.  The waves of a workgroup are independent (no
+// barrier after the prologue); 256 shares the put-mask and period tables
+// (1.6 KB of LDS) between four waves.
+constexpr int kEWG = 256;
+__global__ __launch_bounds__(kEWG) __attribute__((amdgpu_waves_per_eu(5, 8))) void rows_exec_kernel(const uint8_t* __restrict__ src,
                                                        const int64_t* __restrict__ src_off,
                                                        const int32_t* __restrict__ src_len, uint8_t* dst,
                                                        const int64_t* __restrict__ dst_off,
@@ -1016,29 +732,18 @@ __global__ __launch_bounds__(kEWG) __attribute__((amdgpu_waves_per_eu(LZ4M_ROWS_
                                                        const uint8_t* __restrict__ lens, int64_t n,
                                                        unsigned long long* __restrict__ ctr) {
     __shared__ __attribute__((aligned(16))) uint8_t hists[kEWG / 16 * kRowsHS];
-#if LZ4M_LDS_ALIGN
     __shared__ __attribute__((aligned(16))) uint32_t mtab[kPutTab];
-#else
-    __shared__ __attribute__((aligned(16))) uint8_t dums[kEWG * 16];
-#endif
     __shared__ __attribute__((aligned(16))) uint32_t psel[16 * 8];
     __shared__ __attribute__((aligned(16))) u32x4 xsl[kEWG * 2];
     const uint32_t lane = threadIdx.x & 63u;   // lane of the wave
     const int32_t jj = (int32_t)(lane & 15), r = (int32_t)(lane >> 4);
     lds_u8* HB = (lds_u8*)(hists + (threadIdx.x >> 4) * kRowsHS);   // the row's history
-#if LZ4M_LDS_ALIGN
     lds_put_table_init(mtab, threadIdx.x, kEWG);
     lds_cu32* MT = (lds_cu32*)mtab;
-#else
-    lds_u8* DUM = (lds_u8*)(dums + threadIdx.x * 16);
-#endif
     period_sel_init(psel, threadIdx.x, kEWG);
-    if (kEWG > 64) __syncthreads();   // tables written by other waves
+    __syncthreads();   // tables written by other waves
     lds_cu32* PS = (lds_cu32*)psel;
     lds_u32x4* XSL = (lds_u32x4*)(xsl + 2 * threadIdx.x);
-    // this lane's dummy store target (flush stores of lanes with nothing final)
-    uint8_t* const dst_dummy = reinterpret_cast<uint8_t*>(ctr) + kRowsDummy + 1024 * ((blockIdx.x * (kEWG / 64) + (threadIdx.x >> 6)) % kRowsDummySlots) + 16 * lane;
-    (void)dst_dummy;
     // row state (uniform across the row's 16 lanes)
     const uint8_t* s = nullptr;
     uint8_t* d = nullptr;
@@ -1055,9 +760,7 @@ __global__ __launch_bounds__(kEWG) __attribute__((amdgpu_waves_per_eu(LZ4M_ROWS_
     // for it -- in order, for every younger request too: r05)
     int32_t incq = 0, lraw = 0;
     u32x4 na = u32x4{0, 0, 0, 0}, nb = na;
-    RP_DECL
     while (true) {
-        RP_MARK(14);
         if (!have) {
             unsigned long long b = 0;
             if (jj == 0) b = atomicAdd(&ctr[2], 1ull);
@@ -1066,12 +769,7 @@ __global__ __launch_bounds__(kEWG) __attribute__((amdgpu_waves_per_eu(LZ4M_ROWS_
             b = ((unsigned long long)bhi << 32) | blo;
             if (b >= (unsigned long long)n) break;
             const RowMeta mt = meta[b];
-            RP_COUNT(23, 1);
-            if (mt.nseq == 0) {   // the finisher decodes the whole block
-                RP_COUNT(24, 1);
-                RP_MARK(22);
-                continue;
-            }
+            if (mt.nseq == 0) continue;   // the finisher decodes the whole block
             s = src + src_off[b];
             d = dst + dst_off[b];
             iend = src_len[b];
@@ -1080,13 +778,8 @@ __global__ __launch_bounds__(kEWG) __attribute__((amdgpu_waves_per_eu(LZ4M_ROWS_
             k0 = ip = op = base = F = 0;
             have = true;
             sync = true;
-#if LZ4M_ROWS_COUNTED
-            wait_vm0();   // (once per block) no use of the row's state waits on the common path
-#endif
         }
-        RP_MARK(8);
         if (sync) {   // block start, or the last round stopped early: parse this round now
-            RP_COUNT(19, 1);
             const int32_t dc = load_len(dl, k0 + jj, nseq);
             const int32_t tc = ip + row_incl_sum(dc) - dc;
             u32x4 wa, wb;
@@ -1102,19 +795,12 @@ __global__ __launch_bounds__(kEWG) __attribute__((amdgpu_waves_per_eu(LZ4M_ROWS_
             // with the common one made every round wait for its newest
             // far-source request (r05a: -1.7 %)
             wait_vm0();
-#if LZ4M_ROWS_COUNTED
-            wait_vm0();   // (rare: block starts, short rounds) the common path's waits stay counted
-#endif
         }
         if ((P.fl >> 8) == 0) {
             sync = true;
             if (k0 >= nseq) {   // the block's good prefix is done: flush the rest exactly
                 for (int32_t c = F + cold_j16(jj); c < op; c += 256) gbl_put(d + c, lds_ld16(HB + (c - base)), op - c);
                 have = false;
-#if LZ4M_ROWS_COUNTED
-                wait_vm0();
-#endif
-                RP_MARK(20);
                 continue;
             }
             // one sequence that does not fit the buffers: flush, copy it in
@@ -1154,48 +840,27 @@ __global__ __launch_bounds__(kEWG) __attribute__((amdgpu_waves_per_eu(LZ4M_ROWS_
             // op < oend - 64: the 16-byte reads stay inside the block's slot
             for (int32_t c = base + cold_j16(jj); c < op; c += 256) lds_st16(HB + (c - base), ld16(d + c));
             F = op;
-#if LZ4M_ROWS_COUNTED
-            wait_vm0();
-#endif
-            RP_COUNT(25, 1);
-            RP_MARK(21);
             continue;
         }
-        RP_MARK(10);
-        RP_COUNT(16, 1);
-        RP_COUNT(18, __popcll(__ballot((P.fl & kFlU) != 0)));
+        // ---- literals: bytes lp.. of the input (exact); longer ones rare
         {
-        const bool u = (P.fl & kFlU) != 0;
-        const int32_t lit = P.lit, o = P.o;
-        // literals: bytes lp.. of the input (exact, branch-free); longer ones rare
-        if (!(LZ4M_ROWS_XP & 32)) {
-#if LZ4M_LDS_ALIGN
-        if (u && lit > 0) lds_put_al(HB + (o - base), XSL[0], lit, MT);
-#elif LZ4M_ROWS_LITPUT == 1
-        if (u && lit > 0) lds_put_bf(HB + (o - base), DUM, XSL[0], lit);
-#elif LZ4M_ROWS_LITPUT == 2
-        if (u && lit > 0) lds_put_masked(HB + (o - base), XSL[0], lit);
-#else
-        lds_put_bf(HB + (o - base), DUM, XSL[0], u ? lit : 0);
-#endif
-        if (u && lit > 16) {
-            if (!(P.fl & kFlLitHbm)) {
-                LDS_PUT(HB + (o - base + 16), XSL[1], lit - 16);
-            } else {   // a literal beyond the bytes at hand: from HBM (inside the block: good)
-                for (int32_t i = 16; i < lit; i += 16) LDS_PUT(HB + (o - base + i), ld16(s + P.t + i), lit - i);
-#if LZ4M_ROWS_COUNTED
-                wait_vm0();
-#endif
+            const bool u = (P.fl & kFlU) != 0;
+            const int32_t lit = P.lit, o = P.o;
+            if (u && lit > 0) lds_put_al(HB + (o - base), XSL[0], lit, MT);
+            if (u && lit > 16) {
+                if (!(P.fl & kFlLitHbm)) {
+                    LDS_PUT(HB + (o - base + 16), XSL[1], lit - 16);
+                } else {   // a literal beyond the bytes at hand: from HBM (inside the block: good)
+                    for (int32_t i = 16; i < lit; i += 16) LDS_PUT(HB + (o - base + i), ld16(s + P.t + i), lit - i);
+                }
             }
         }
-        }
-        }
-        // ---- parse the next round ahead (its far sources are requested now),
-        // then request the inputs of the round after it.  LZ4M_ROWS_ORDER 1:
-        // after this round's passes, so that no load the passes wait on (a
+        // ---- the next round, parsed ahead (its far sources are requested
+        // then), and the inputs of the round after it are requested: after
+        // this round's passes (below), so that no load the passes wait on (a
         // long far match's later pieces, a late source) is younger than these
         // requests -- gfx9 counts loads in order, and waiting for one load
-        // waits for every older one
+        // waits for every older one (r05)
         const bool ahead = (P.fl >> 8) == 16 && k0 + 16 < nseq;
         auto parse_ahead = [&]() __attribute__((always_inline)) {
             if (ahead) {
@@ -1208,24 +873,18 @@ __global__ __launch_bounds__(kEWG) __attribute__((amdgpu_waves_per_eu(LZ4M_ROWS_
                 lraw = load_len(dl, k0 + 48 + jj, nseq);
             }
         };
-        if (!LZ4M_ROWS_ORDER) parse_ahead();
-        RP_MARK(11);
         // ---- execute round P
         const bool u = (P.fl & kFlU) != 0;
         const int32_t lit = P.lit, off = P.off, ml = P.ml, o = P.o;
         const int32_t m = o + lit, mend = m + ml, s0 = m - off;
-        RP_MARK(12);
         // readiness passes: a match is copied once no earlier pending match of
         // the round writes into its source [s0, se)
         const bool far = (P.fl & kFlFar) != 0, late = (P.fl & kFlLate) != 0;
         u32x4 g0 = FS.g0;
         const u32x4 g1 = FS.g1;
-        if (!(LZ4M_ROWS_XP & 4) && __any(late)) {   // a source flushed only by the previous round (rare): load it now
+        if (__any(late)) {   // a source flushed only by the previous round (rare): load it now
             const u32x4 lv = ld16(d + (late ? s0 : 0));
             g0 = late ? lv : g0;
-#if LZ4M_ROWS_COUNTED
-            wait_vm0();
-#endif
         }
         const int32_t se = s0 + (off < ml ? off : ml);
         const bool per = off < 16;   // period pattern (s0 >= base here: m - base >= off)
@@ -1236,27 +895,13 @@ __global__ __launch_bounds__(kEWG) __attribute__((amdgpu_waves_per_eu(LZ4M_ROWS_
                                     (5ull << 33) | (4ull << 36) | (3ull << 39) | (2ull << 42) | (1ull << 45);
         const int32_t stp = per ? 16 - (int32_t)((kRem16 >> (3u * ((uint32_t)off & 15u))) & 7u) : 16;
         bool pend = u;
-#if LZ4M_ROWS_FARXS
-        // a far source's two pieces wait in the lane's literal slot (the
-        // literals are placed; the next round's parse refills the slot after
-        // the passes), so that a copy reads every source from LDS by address
-        if (far) XSL[0] = g0;
-        if (far & !late & (ml > 16)) XSL[1] = g1;
-        const lds_u8* const farp = (const lds_u8*)XSL;
-#endif
-#if LZ4M_ROWS_PUTMASK >= 3
         // one match copy (exec-masked to the ready lanes: an LDS access costs per active lane)
         auto copy_match = [&]() __attribute__((always_inline)) {
-#if LZ4M_ROWS_FARXS
-            const u32x4 l0 = lds_ld16u(far ? farp : HB + (s0 >= base ? s0 - base : 0));
-            u32x4 v0 = l0;
-#else
-            const u32x4 l0 = (LZ4M_ROWS_XP & 2048) ? u32x4{(uint32_t)s0, 0u, 0u, 0u} : lds_ld16u(HB + (s0 >= base ? s0 - base : 0));
+            const u32x4 l0 = lds_ld16a(HB + (s0 >= base ? s0 - base : 0));
             u32x4 v0 = far ? g0 : l0;
-#endif
             if (per) v0 = period_perm(l0, PS + 8 * off);
-            if (!(LZ4M_ROWS_XP & 1024)) LDS_PUT(HB + (m - base), v0, ml);
-            if (ml > stp && !(LZ4M_ROWS_XP & 512)) {   // the rest (matches longer than one step)
+            LDS_PUT(HB + (m - base), v0, ml);
+            if (ml > stp) {   // the rest (matches longer than one step)
                 for (int32_t i = stp; i < ml; i += stp) {
                     u32x4 v = v0;
                     if (!per) {
@@ -1265,104 +910,33 @@ __global__ __launch_bounds__(kEWG) __attribute__((amdgpu_waves_per_eu(LZ4M_ROWS_
                         // second piece of a (not late) far source was requested
                         // with the first; later pieces are loaded now, only where
                         // some lane needs one (this wait then covers only loads
-                        // older than the round's own requests, LZ4M_ROWS_ORDER)
-#if LZ4M_ROWS_FARXS
+                        // older than the round's own requests)
+                        v = lds_ld16a(HB + (sp >= base ? sp - base : 0));
                         const bool pc1 = (i == 16) & far & !late;
-                        v = lds_ld16u((sp < base) & pc1 ? farp + 16 : HB + (sp >= base ? sp - base : 0));
-                        {
-#else
-                        v = (LZ4M_ROWS_XP & 2048) ? u32x4{(uint32_t)sp, 0u, 0u, 0u} : lds_ld16u(HB + (sp >= base ? sp - base : 0));
-                        if (!(LZ4M_ROWS_XP & 2)) {
-                            const bool pc1 = (i == 16) & far & !late;
-                            if (sp < base && pc1) v = g1;
-#endif
-                            const bool hb = (sp < base) & !pc1;
-                            if (__any(hb)) {
-                                const u32x4 x = ld16(d + (hb ? sp : 0));
-                                v = hb ? x : v;
-                            }
+                        if (sp < base && pc1) v = g1;
+                        const bool hb = (sp < base) & !pc1;
+                        if (__any(hb)) {
+                            const u32x4 x = ld16(d + (hb ? sp : 0));
+                            v = hb ? x : v;
                         }
                     }
-                    if (!(LZ4M_ROWS_XP & 1024)) LDS_PUT(HB + (m - base + i), v, ml - i);
+                    LDS_PUT(HB + (m - base + i), v, ml - i);
                 }
             }
         };
-#if LZ4M_ROWS_PASS1
-        // the first pass needs no scan: a match whose source lies wholly
-        // before the round's output (most of them) reads final bytes
-        {
-            RP_COUNT(17, 1);
-            const bool ready = pend & (se <= row_first(o));
-            if (ready) copy_match();
-            pend = pend && !ready;
-        }
-#endif
-#endif
         while (__any(pend)) {
-            RP_COUNT(17, 1);
             // x1 = 1 + the end of the nearest pending match below, y1 = BIG -
             // the start of the first pending match below (0: none)
             int32_t x1, y1;
             row_excl_max2(pend ? mend + 1 : 0, pend ? 0x3FFFFFFF - m : 0, x1, y1);
-            const bool ready = (LZ4M_ROWS_XP & 16) ? pend : pend & ((x1 <= s0 + 1) | (y1 <= 0x3FFFFFFF - se));
-#if LZ4M_ROWS_PUTMASK >= 3
-            if (ready && !(LZ4M_ROWS_XP & 128)) copy_match();
+            const bool ready = pend & ((x1 <= s0 + 1) | (y1 <= 0x3FFFFFFF - se));
+            if (ready) copy_match();
             pend = pend && !ready;
         }
-#else
-            // first 16 bytes: branch-free
-            const u32x4 l0 = lds_ld16u(HB + (s0 >= base ? s0 - base : 0));
-            u32x4 v0 = far ? g0 : l0;
-            if (__any(ready && per)) {
-                const u32x4 pp = period_perm(l0, PS + 8 * (per ? off : 0));
-                v0 = per ? pp : v0;
-            }
-#if LZ4M_ROWS_PUTMASK >= 1
-            if (ready) lds_put(HB + (m - base), v0, ml);
-#else
-            lds_put_bf(HB + (m - base), DUM, v0, ready ? ml : 0);
-#endif
-            // the rest (matches longer than one step)
-            if (ready && ml > stp) {
-                for (int32_t i = stp; i < ml; i += stp) {
-                    u32x4 v;
-                    if (per) {
-                        v = v0;
-                    } else {
-                        const int32_t sp = s0 + i;
-                        // sp < base: flushed (F >= base + kRowsKeep - 16)
-                        v = sp >= base ? lds_ld16u(HB + (sp - base)) : ld16(d + sp);
-                    }
-                    lds_put(HB + (m - base + i), v, ml - i);
-                }
-            }
-            pend = pend && !ready;
-        }
-#endif
-        RP_MARK(13);
-        if (LZ4M_ROWS_ORDER) parse_ahead();
-        RP_MARK(15);
+        parse_ahead();
         // ---- flush, advance, rebase for the next round
         const int32_t opn = P.opn;
-#if LZ4M_ROWS_COUNTED
-        // exactly one store per lane and round, always issued (a lane with no
-        // complete chunk stores to its dummy slot), so the compiler counts the
-        // next round's waits instead of draining these stores (gfx9 counts
-        // stores in vmcnt); more than 256 pending bytes in a row is rare
-        {
-            const int32_t c = F + 16 * jj;
-            const bool fin = c + 16 <= opn;
-            const u32x4 v = lds_ld16(HB + (fin ? c - base : 0));
-            st16(fin ? d + c : dst_dummy, v);
-            if (__any(F + 256 + 16 <= opn)) {
-                for (int32_t c2 = c + 256; c2 + 16 <= opn; c2 += 256) st16(d + c2, lds_ld16(HB + (c2 - base)));
-                wait_vm0();
-            }
-        }
-#else
-        if (!(LZ4M_ROWS_XP & 64))
-            for (int32_t c = F + 16 * jj; c + 16 <= opn; c += 256) st16(d + c, lds_ld16(HB + (c - base)));
-#endif
+        for (int32_t c = F + 16 * jj; c + 16 <= opn; c += 256) st16(d + c, lds_ld16(HB + (c - base)));
         F += (opn - F) & ~15;
         op = opn;
         ip = P.ipn;
@@ -1371,7 +945,7 @@ __global__ __launch_bounds__(kEWG) __attribute__((amdgpu_waves_per_eu(LZ4M_ROWS_
         if (nbse != base) {
             // the kept bytes lie >= kRowsH - kRowsRoom - kRowsKeep past the
             // buffer start: all reads of a group before its writes
-            for (int32_t c0 = 0; c0 < ((LZ4M_ROWS_XP & 256) ? 0 : op - nbse); c0 += 1024) {
+            for (int32_t c0 = 0; c0 < op - nbse; c0 += 1024) {
                 u32x4 v[4];
 #pragma unroll
                 for (int g = 0; g < 4; ++g) v[g] = lds_ld16(HB + (nbse - base) + c0 + 256 * g + 16 * jj);
@@ -1385,25 +959,13 @@ __global__ __launch_bounds__(kEWG) __attribute__((amdgpu_waves_per_eu(LZ4M_ROWS_
         } else {
             sync = true;
         }
-        RP_MARK(9);
     }
-    RP_FLUSH(8, 32);
 }
 
 }  // namespace lz4m
 
 using namespace lz4m;
 
-#ifdef LZ4M_ROWS_PROF
-extern "C" int lz4m_rows_prof(unsigned long long* out, int reset) {
-    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(lz4m::g_rows_prof), sizeof(unsigned long long) * 32);
-    if (e == hipSuccess && reset) {
-        unsigned long long z[32] = {0};
-        e = hipMemcpyToSymbol(HIP_SYMBOL(lz4m::g_rows_prof), z, sizeof(z));
-    }
-    return (int)e;
-}
-#endif
 
 extern "C" size_t lz4m_rows_fixed_bytes(int64_t n) { return kRowsMeta + (size_t)n * sizeof(RowMeta); }
 
