@@ -266,13 +266,10 @@ struct Chunk {
     uint32_t bp, bc;  // 4 bytes before p / before cand
 };
 
-// LZ4M_PC_XCHG: each lane exchanges its position into its bucket and reads
-// back the entry before it; one instruction's lanes on one LDS address are
-// applied in lane order on gfx950 (tools/micro/lds_xchg_order.hip, r05l), so
-// that is the most recent earlier position with the same hash -- the
-// candidate -- and the table ends holding each bucket's last position, as
-// with the per-hash-bit ballots it replaces.  r05n: 0.8 % slower than the
-// ballots (the 16-bit form's return needs an explicit LDS wait), so off.
+// (Measured and not kept, r05n: each lane exchanging its position into its
+// bucket -- the lanes of one LDS instruction applied in lane order, as the
+// exact compressor's search step does -- in place of the per-hash-bit
+// ballots: 0.8 % slower, the 16-bit form's return needing an explicit wait.)
 
 // WIN (blocks > 64 KiB): the table holds the low 16 bits of each position
 // (u16, as for blocks <= 64 KiB) instead of whole u32 positions, and a
@@ -285,7 +282,6 @@ template <bool BIG, int HB, bool WIN = false>
 __device__ __forceinline__ void chunk_issue(Chunk& C, const uint8_t* s, uint32_t* table32, int32_t p0, uint32_t v,
                                             int32_t N, int32_t mlast, uint32_t lane) {
     constexpr bool U32 = BIG && !WIN;   // whole positions in a u32 table
-    static_assert(!(0 && WIN), "the exchange variant has no windowed table");
     const int32_t p = p0 + (int32_t)lane;
     const bool act = p + 4 <= N;
     const uint32_t h = act ? phash<HB>(v) : (1u << HB);

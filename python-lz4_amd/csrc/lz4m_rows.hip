@@ -50,6 +50,18 @@ __device__ __forceinline__ int32_t row_incl_sum(int32_t v) {
     v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);   // row_shr:8
     return v;
 }
+// two inclusive row prefix sums at once (the chains interleave: no wait
+// states between dependent DPP steps)
+__device__ __forceinline__ void row_incl_sum2(int32_t& a, int32_t& b) {
+    a += __builtin_amdgcn_update_dpp(0, a, 0x111, 0xF, 0xF, false);
+    b += __builtin_amdgcn_update_dpp(0, b, 0x111, 0xF, 0xF, false);
+    a += __builtin_amdgcn_update_dpp(0, a, 0x112, 0xF, 0xF, false);
+    b += __builtin_amdgcn_update_dpp(0, b, 0x112, 0xF, 0xF, false);
+    a += __builtin_amdgcn_update_dpp(0, a, 0x114, 0xF, 0xF, false);
+    b += __builtin_amdgcn_update_dpp(0, b, 0x114, 0xF, 0xF, false);
+    a += __builtin_amdgcn_update_dpp(0, a, 0x118, 0xF, 0xF, false);
+    b += __builtin_amdgcn_update_dpp(0, b, 0x118, 0xF, 0xF, false);
+}
 __device__ __forceinline__ int32_t row_last(int32_t v) { return __builtin_amdgcn_update_dpp(0, v, 0x15F, 0xF, 0xF, false); }
 __device__ __forceinline__ int32_t row_first(int32_t v) { return __builtin_amdgcn_update_dpp(0, v, 0x150, 0xF, 0xF, false); }
 
@@ -514,13 +526,6 @@ __global__ __launch_bounds__(kPWG) void rows_parse_kernel(const uint8_t* __restr
 // the 32 bytes of the NEXT round are requested while this round copies, so a
 // round waits on at most one memory round trip (its far match sources).
 constexpr int32_t kRowsH = 1024;   // history per row (bytes): 1 KiB measured as fast as 2 KiB at equal occupancy
-#ifndef LZ4M_ROWS_OFFLDS
-// 1: the match offset read back from the literal's LDS slot (72 VALU fewer
-// in the kernel).  r05q: the first rows test ended in an illegal memory
-// access with it on; cause not found (the ISA's offsets match the select
-// form's), so it stays off and is not run again until it is
-#define LZ4M_ROWS_OFFLDS 0
-#endif
 constexpr int32_t kRowsHS = kRowsH + 32;   // buffer stride (16-byte reads past the end stay inside)
 constexpr int32_t kRowsKeep = kRowsH / 2;   // history kept on a rebase
 constexpr int32_t kRowsRoom = 512;          // rebase when less room than this is left
@@ -559,6 +564,13 @@ __device__ __forceinline__ void load32(const uint8_t* s, int32_t t, int32_t iend
 }
 
 
+#define LDS_PUT(p, v, k) lds_put_al((p), (v), (k), MT)
+
+// Offsets inside a block's slots are never negative, so a 64-bit address is
+// the base plus a zero-extended offset (no sign extension and no select of its
+// high half per load; r06f: -0.6 % with the interleaved row sums below)
+#define ROFF(x) ((uint32_t)(x))
+
 // One round of a row, parsed: lane jj's sequence (literal at input position
 // t, lit / off / ml), its output position o, the round's row totals and the
 // far source requested from HBM; the literal's first 32 bytes go to XS.
@@ -590,7 +602,7 @@ struct FarSrc {
 __device__ __forceinline__ void parse_round(PSeq& P, int32_t jj, int32_t r, int32_t k0, int32_t nseq, int32_t ip,
                                             int32_t op, int32_t bnext, int32_t F, const uint8_t* s, const uint8_t* d,
                                             int32_t iend, int32_t dlt, int32_t t, u32x4 wa, u32x4 wb, lds_u32x4* XS,
-                                            FarSrc& FS) {
+                                            FarSrc& FS, int32_t& incsum) {
     const bool act = k0 + jj < nseq;
     const bool esc = dlt == 255;   // length >= 255: the parse left it to be re-parsed
     const bool wbok = t + 32 <= iend;
@@ -602,23 +614,6 @@ __device__ __forceinline__ void parse_round(PSeq& P, int32_t jj, int32_t r, int3
     const int32_t po = lp + lit;
     const int32_t mlc = (int32_t)(tok & 15u);
     // offset and first match-length byte: from wa for lit <= 12, else from wa|wb
-#if LZ4M_ROWS_OFFLDS
-    // (the literal's 32 bytes go to the lane's LDS slot first; the offset is
-    // its byte lit: two aligned dwords read back and one alignbyte, instead of
-    // selecting among the 8 dwords of wa|wb)
-    const uint32_t sh = (uint32_t)lp;
-    XS[0] = u32x4{__builtin_amdgcn_alignbyte(wa.y, wa.x, sh), __builtin_amdgcn_alignbyte(wa.z, wa.y, sh),
-                 __builtin_amdgcn_alignbyte(wa.w, wa.z, sh), __builtin_amdgcn_alignbyte(wb.x, wa.w, sh)};
-    XS[1] = u32x4{__builtin_amdgcn_alignbyte(wb.y, wb.x, sh), __builtin_amdgcn_alignbyte(wb.z, wb.y, sh),
-                 __builtin_amdgcn_alignbyte(wb.w, wb.z, sh), __builtin_amdgcn_alignbyte(0u, wb.w, sh)};
-    const uint32_t lq = (uint32_t)(lit < 28 ? lit : 28);
-    const lds_cu32a* xd = (const lds_cu32a*)XS;
-    const uint32_t q0 = lq >> 2, q1 = q0 < 7u ? q0 + 1u : 7u;   // (lq = 28: one dword, shift 0)
-    const uint32_t dwo = __builtin_amdgcn_alignbyte(xd[q1], xd[q0], lq & 3u);
-    // (lit > 29: the offset lies past the 32 bytes, `slow` re-reads it: any
-    // shift in 0..31 will do -- a wider one would be undefined)
-    const uint32_t bsh = lit > 28 ? 8u : 0u;
-#else
     // the dword pair at pq selected by a tree on its three index bits (14
     // selects) for every lane, instead of a 16-byte and a 32-byte select chain
     // both computed and selected between
@@ -627,7 +622,6 @@ __device__ __forceinline__ void parse_round(PSeq& P, int32_t jj, int32_t r, int3
     // (po > 29: past the 32 bytes, `slow` re-reads the offset: any shift in
     // 0..31 will do -- 8 * (po - pq) would reach 32 and be undefined)
     const uint32_t bsh = po > 28 ? 8u : 0u;
-#endif
     int32_t off = (int32_t)((dwo >> bsh) & 0xFFFFu);
     const int32_t e0 = (int32_t)((dwo >> (bsh + 16)) & 0xFFu);
     int32_t ml = mlc + (mlc == 15 ? e0 : 0);
@@ -648,17 +642,24 @@ __device__ __forceinline__ void parse_round(PSeq& P, int32_t jj, int32_t r, int3
     }
     ml += 4;
     const int32_t len = act && !esc ? lit + ml : 0;
-    const int32_t o = op + row_incl_sum(len) - len;
+    // (with the next round's length-byte prefix sum, incsum: two chains)
+    int32_t lsum = len;
+    row_incl_sum2(lsum, incsum);
+    const int32_t o = op + lsum - len;
     const int32_t mend = o + lit + ml;
     const bool ok = act & !esc & (mend <= bnext + kRowsH);
     const uint64_t nok = __ballot(!ok);
-    const uint32_t rb = (uint32_t)(nok >> (16 * r)) & 0xFFFFu;
-    const int32_t use = rb ? __builtin_ctz(rb) : 16;
-    const bool u = jj < use;
+    int32_t use;
+    bool u;
     if (nok == 0) {   // every row takes its 16 sequences: the ends of lane 15's
+        use = 16;
+        u = true;
         P.opn = row_last(o + len);
         P.ipn = row_last(t + dlt);
     } else {
+        const uint32_t rb = (uint32_t)(nok >> (16 * r)) & 0xFFFFu;
+        use = rb ? __builtin_ctz(rb) : 16;
+        u = jj < use;
         P.opn = op + row_last(row_incl_sum(u ? len : 0));
         P.ipn = ip + row_last(row_incl_sum(u ? dlt : 0));
     }
@@ -667,16 +668,14 @@ __device__ __forceinline__ void parse_round(PSeq& P, int32_t jj, int32_t r, int3
     const bool late = far & (s0 + 32 > F);
     const bool pf = far & !late;
     // unconditional requests (lanes without a far source read the block start)
-    FS.g0 = ld16(d + (pf ? s0 : 0));
+    FS.g0 = ld16(d + ROFF(pf ? s0 : 0));
     // the second piece [s0 + 16, s0 + 32) is flushed too (not late: s0 + 32 <= F)
-    FS.g1 = ld16(d + ((pf & (ml > 16)) ? s0 + 16 : 0));
-#if !LZ4M_ROWS_OFFLDS
+    FS.g1 = ld16(d + ROFF((pf & (ml > 16)) ? s0 + 16 : 0));
     const uint32_t sh = (uint32_t)lp;
     XS[0] = u32x4{__builtin_amdgcn_alignbyte(wa.y, wa.x, sh), __builtin_amdgcn_alignbyte(wa.z, wa.y, sh),
                  __builtin_amdgcn_alignbyte(wa.w, wa.z, sh), __builtin_amdgcn_alignbyte(wb.x, wa.w, sh)};
     XS[1] = u32x4{__builtin_amdgcn_alignbyte(wb.y, wb.x, sh), __builtin_amdgcn_alignbyte(wb.z, wb.y, sh),
                  __builtin_amdgcn_alignbyte(wb.w, wb.z, sh), __builtin_amdgcn_alignbyte(0u, wb.w, sh)};
-#endif
     P.t = t + lp;
     P.lit = lit;
     P.off = off;
@@ -704,17 +703,16 @@ __device__ __forceinline__ int32_t next_base(int32_t op, int32_t base) {
 __device__ __forceinline__ void load_in(const uint8_t* s, int32_t t, int32_t iend, u32x4& a, u32x4& b) {
     const int32_t ta = t + 16 <= iend ? t : 0;   // good sequences: t + 16 < iend
     const int32_t tb = t + 32 <= iend ? t + 16 : iend - 16;
-    a = ld16(s + ta);
-    b = ld16(s + tb);
+    a = ld16(s + ROFF(ta));
+    b = ld16(s + ROFF(tb));
 }
 // (no select on the loaded value: a lane past the block's good sequences
 // reads the last length, and parse_round masks it by `act`; a select here
 // waited for the load at once)
 __device__ __forceinline__ int32_t load_len(const uint8_t* dl, int32_t k, int32_t nseq) {
-    return (int32_t)dl[k < nseq ? k : nseq - 1];
+    return (int32_t)dl[ROFF(k < nseq ? k : nseq - 1)];
 }
 
-#define LDS_PUT(p, v, k) lds_put_al((p), (v), (k), MT)
 
 // Rows in flight: round R executes while round R + 1 is already parsed
 // (its far sources in flight) and round R + 2's inputs are requested, so a
@@ -784,7 +782,8 @@ __global__ __launch_bounds__(kEWG) __attribute__((amdgpu_waves_per_eu(5, 8))) vo
             const int32_t tc = ip + row_incl_sum(dc) - dc;
             u32x4 wa, wb;
             load_in(s, tc, iend, wa, wb);
-            parse_round(P, jj, r, k0, nseq, ip, op, base, F, s, d, iend, dc, tc, wa, wb, XSL, FS);
+            int32_t dummy = 0;
+            parse_round(P, jj, r, k0, nseq, ip, op, base, F, s, d, iend, dc, tc, wa, wb, XSL, FS, dummy);
             const int32_t dq = load_len(dl, k0 + 16 + jj, nseq);
             incq = row_incl_sum(dq);
             load_in(s, P.ipn + incq - dq, iend, na, nb);
@@ -846,7 +845,7 @@ __global__ __launch_bounds__(kEWG) __attribute__((amdgpu_waves_per_eu(5, 8))) vo
         {
             const bool u = (P.fl & kFlU) != 0;
             const int32_t lit = P.lit, o = P.o;
-            if (u && lit > 0) lds_put_al(HB + (o - base), XSL[0], lit, MT);
+            if (u && lit > 0) LDS_PUT(HB + (o - base), XSL[0], lit);
             if (u && lit > 16) {
                 if (!(P.fl & kFlLitHbm)) {
                     LDS_PUT(HB + (o - base + 16), XSL[1], lit - 16);
@@ -867,8 +866,9 @@ __global__ __launch_bounds__(kEWG) __attribute__((amdgpu_waves_per_eu(5, 8))) vo
                 const int32_t bq = next_base(P.opn, base);
                 // Q's length bytes from their prefix sum: lane j's minus lane j-1's
                 const int32_t dq = incq - __builtin_amdgcn_update_dpp(0, incq, 0x111, 0xF, 0xF, true);
-                parse_round(Q, jj, r, k0 + 16, nseq, P.ipn, P.opn, bq, F, s, d, iend, dq, P.ipn + incq - dq, na, nb, XSL, FS);
-                incq = row_incl_sum(lraw);
+                int32_t inc2 = lraw;
+                parse_round(Q, jj, r, k0 + 16, nseq, P.ipn, P.opn, bq, F, s, d, iend, dq, P.ipn + incq - dq, na, nb, XSL, FS, inc2);
+                incq = inc2;
                 load_in(s, Q.ipn + incq - lraw, iend, na, nb);
                 lraw = load_len(dl, k0 + 48 + jj, nseq);
             }
@@ -883,7 +883,7 @@ __global__ __launch_bounds__(kEWG) __attribute__((amdgpu_waves_per_eu(5, 8))) vo
         u32x4 g0 = FS.g0;
         const u32x4 g1 = FS.g1;
         if (__any(late)) {   // a source flushed only by the previous round (rare): load it now
-            const u32x4 lv = ld16(d + (late ? s0 : 0));
+            const u32x4 lv = ld16(d + ROFF(late ? s0 : 0));
             g0 = late ? lv : g0;
         }
         const int32_t se = s0 + (off < ml ? off : ml);
@@ -916,7 +916,7 @@ __global__ __launch_bounds__(kEWG) __attribute__((amdgpu_waves_per_eu(5, 8))) vo
                         if (sp < base && pc1) v = g1;
                         const bool hb = (sp < base) & !pc1;
                         if (__any(hb)) {
-                            const u32x4 x = ld16(d + (hb ? sp : 0));
+                            const u32x4 x = ld16(d + ROFF(hb ? sp : 0));
                             v = hb ? x : v;
                         }
                     }
@@ -936,7 +936,7 @@ __global__ __launch_bounds__(kEWG) __attribute__((amdgpu_waves_per_eu(5, 8))) vo
         parse_ahead();
         // ---- flush, advance, rebase for the next round
         const int32_t opn = P.opn;
-        for (int32_t c = F + 16 * jj; c + 16 <= opn; c += 256) st16(d + c, lds_ld16(HB + (c - base)));
+        for (int32_t c = F + 16 * jj; c + 16 <= opn; c += 256) st16(d + ROFF(c), lds_ld16(HB + (c - base)));
         F += (opn - F) & ~15;
         op = opn;
         ip = P.ipn;
@@ -952,6 +952,8 @@ __global__ __launch_bounds__(kEWG) __attribute__((amdgpu_waves_per_eu(5, 8))) vo
 #pragma unroll
                 for (int g = 0; g < 4; ++g) lds_st16(HB + c0 + 256 * g + 16 * jj, v[g]);
             }
+            // (the copy moved 1 KiB: bytes past op - nbse came from past the
+            // old output, zero, or from past the row's buffer)
             base = nbse;
         }
         if (ahead) {
