@@ -1,6 +1,6 @@
 """Dev probe: config 4's device frame compress without a content checksum
 (8 GiB, 4 MiB independent blocks, parallel parse): the whole call against
-its compression launch alone, and the compressed size (LZ4M_PC_LARGE / LZ4M_PC_SEG / LZ4M_PC_SEGHB A/B)."""
+its compression launch alone, and the compressed size (LZ4M_PC_SEG A/B; the LZ4M_PC_LARGE / LZ4M_PC_SEGHB knobs left the sources in round 6)."""
 import os
 import sys
 import time
