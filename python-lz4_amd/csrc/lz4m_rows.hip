@@ -128,15 +128,6 @@ __device__ __forceinline__ void gbl_put(uint8_t* p, u32x4 v, int32_t k) {
     if (k & 1) p[o] = (uint8_t)window_dword(v, o);
 }
 
-// The 4 bytes at byte k (0..15) of w (bytes past 15 read as zero), with
-// selects only (no branches).
-__device__ __forceinline__ uint32_t dword_at(u32x4 w, uint32_t k) {
-    const bool b4 = (k & 4) != 0, b8 = (k & 8) != 0;
-    const uint32_t a0 = b4 ? w.y : w.x, a1 = b4 ? w.z : w.y, a2 = b4 ? w.w : w.z, a3 = b4 ? 0u : w.w;
-    const uint32_t lo = b8 ? a2 : a0, hi = b8 ? a3 : a1;
-    return __builtin_amdgcn_alignbyte(hi, lo, k & 3);
-}
-
 // the 4 bytes at k (0..28) of the 32-byte window a|b, the dwords selected by
 // a tree on the index bits
 __device__ __forceinline__ uint32_t dword32_tree(u32x4 a, u32x4 b, uint32_t k) {
@@ -151,13 +142,6 @@ __device__ __forceinline__ uint32_t dword32_tree(u32x4 a, u32x4 b, uint32_t k) {
     return __builtin_amdgcn_alignbyte(hi, lo, k & 3);
 }
 
-// the 4 bytes at k (0..28) of the 32-byte window a|b
-__device__ __forceinline__ uint32_t dword32(u32x4 a, u32x4 b, uint32_t k) {
-    const uint32_t q = k >> 2;
-    const uint32_t lo = q == 0 ? a.x : q == 1 ? a.y : q == 2 ? a.z : q == 3 ? a.w : q == 4 ? b.x : q == 5 ? b.y : q == 6 ? b.z : b.w;
-    const uint32_t hi = q == 0 ? a.y : q == 1 ? a.z : q == 2 ? a.w : q == 3 ? b.x : q == 4 ? b.y : q == 5 ? b.z : q == 6 ? b.w : 0u;
-    return __builtin_amdgcn_alignbyte(hi, lo, k & 3);
-}
 
 // ------------------------------------------------------------ 1. the parse
 // One lane per block.  The compressed block is read through a 128-byte LDS
@@ -165,30 +149,21 @@ __device__ __forceinline__ uint32_t dword32(u32x4 a, u32x4 b, uint32_t k) {
 // 16-byte read wraps per aligned 8-byte piece), and the
 // next 64 bytes [wb + 128, wb + 192) are requested ahead into registers.  The
 // inner loop is the common sequence only -- literal <= 12 bytes, at most one
-// match-length byte, inside the ring, good -- as straight-line code (one
-// 16-byte LDS read, ~30 VALU).  A lane that meets anything else (the ring's
+// match-length byte, inside the ring, good -- as straight-line code: the
+// token byte, then the aligned dword pair holding offset and length byte (two
+// dependent LDS reads, ~30 VALU and ~9 SALU per step; the round-5 step read
+// 16 bytes and selected from them: ~65 VALU, ~33 SALU, r06l/m: 24.3 -> 20.1
+// ms per 1 M probe blocks).  A lane that meets anything else (the ring's
 // end, a longer literal or length, a full length stage, the block's end)
-// waits; once too few lanes can go on, the wave runs one general step: every
+// stops; once too few lanes go on, the wave runs one general step: every
 // lane past the first half of its ring rotates the requested bytes in and
 // requests the next 64, waiting lanes parse one sequence with the general
 // parse.  Recorded lengths are staged in a 32-entry LDS ring per lane and
 // leave for HBM 16 at a time.  The ring refills are loaded by four lanes per
 // block (one 64-byte request instead of four 16-byte ones).
 constexpr int kPW = 128;                // ring bytes
-// 16 ring bytes at ring offset x (0..kPW-1)
-__device__ __forceinline__ u32x4 ring_ld16(const lds_u8* W, int32_t x) {
-    // three aligned 8-byte reads, each wrapped into the ring, and a funnel shift
-    const uint32_t a = (uint32_t)x & ~7u;
-    const uint64_t x0 = *(const lds_vu64*)(W + a), x1 = *(const lds_vu64*)(W + ((a + 8u) & (kPW - 1))),
-                   x2 = *(const lds_vu64*)(W + ((a + 16u) & (kPW - 1)));
-    const bool h = (x & 4) != 0;
-    const uint32_t r = (uint32_t)x & 3u;
-    const uint32_t c0 = (uint32_t)x0, c1 = (uint32_t)(x0 >> 32), c2 = (uint32_t)x1, c3 = (uint32_t)(x1 >> 32),
-                   c4 = (uint32_t)x2, c5 = (uint32_t)(x2 >> 32);
-    const uint32_t e0 = h ? c1 : c0, e1 = h ? c2 : c1, e2 = h ? c3 : c2, e3 = h ? c4 : c3, e4 = h ? c5 : c4;
-    return u32x4{__builtin_amdgcn_alignbyte(e1, e0, r), __builtin_amdgcn_alignbyte(e2, e1, r),
-                 __builtin_amdgcn_alignbyte(e3, e2, r), __builtin_amdgcn_alignbyte(e4, e3, r)};
-}
+typedef __attribute__((address_space(3))) volatile uint8_t lds_vu8;
+typedef __attribute__((address_space(3))) volatile uint32_t lds_vu32;
 constexpr int kPStage = 32;   // length ring (flushed in halves)
 constexpr int kPWG = 64;      // parse workgroup (LDS is allocated per workgroup)
 // a 64-bit address received from another lane, as a global pointer
@@ -198,6 +173,7 @@ __device__ __forceinline__ const uint8_t* readlane_safe_ptr(uint64_t a) {
 }
 constexpr int32_t kPRunCap = 16;        // length-byte runs longer than this end the good prefix (finisher)
 constexpr int kPMinActive = 40;         // run the general step once fewer lanes than this can go on
+constexpr int kPSteps = 4;              // fast steps per count of the lanes going (r06m: 20.60 ms, 2: 20.64)
 
 // 64 stream bytes into ring half h (0: offsets 0-63; 1: 64-127)
 __device__ __forceinline__ void ring_put(lds_u8* W, int32_t h, const u32x4* v) {
@@ -219,11 +195,13 @@ __global__ __launch_bounds__(kPWG) void rows_parse_kernel(const uint8_t* __restr
                                                          const int32_t* __restrict__ dst_cap, int64_t n,
                                                          RowMeta* __restrict__ meta, uint8_t* __restrict__ lens,
                                                          int64_t lens_cap, unsigned long long* __restrict__ ctr) {
-    __shared__ __attribute__((aligned(16))) uint8_t wins[kPWG * kPW];
-    __shared__ __attribute__((aligned(16))) uint8_t stgs[kPWG * kPStage];
+    __shared__ __attribute__((aligned(kPW))) uint8_t wins[kPWG * kPW];
+    __shared__ __attribute__((aligned(kPStage))) uint8_t stgs[kPWG * kPStage];
     const uint32_t lane = lane_id();
     lds_u8* W = (lds_u8*)(wins + threadIdx.x * kPW);
+    const uint32_t Wa = (uint32_t)(uintptr_t)W;   // kPW-aligned: ring offsets are OR-ed in
     lds_u8* stg = (lds_u8*)(stgs + threadIdx.x * kPStage);
+    const uint32_t Sa = (uint32_t)(uintptr_t)stg;   // (kPStage-aligned)
     const uint8_t* s = nullptr;
     int64_t idx = -1, loff = 0;
     int32_t iend = 0, oend = 0, ip = 0, op = 0, k = 0, kf = 0, wb = 0;
@@ -342,8 +320,12 @@ __global__ __launch_bounds__(kPWG) void rows_parse_kernel(const uint8_t* __restr
             // only what this cannot (a 255 extension byte, a literal of more
             // than 27 bytes)
             {
-                const u32x4 w0 = ring_ld16(W, ip & (kPW - 1)), w1 = ring_ld16(W, (ip + 16) & (kPW - 1));
-                const uint32_t tok = w0.x & 0xFFu;
+                // the token and the literal-length byte from the aligned dword
+                // pair at ip, the offset and match-length byte from the pair at
+                // ip + po (po <= 29: inside the 32 bytes the ring holds)
+                const uint32_t x0 = __builtin_amdgcn_alignbyte(*(lds_vu32*)(size_t)(Wa | (((uint32_t)ip + 4u) & (kPW - 4))),
+                                                               *(lds_vu32*)(size_t)(Wa | ((uint32_t)ip & (kPW - 4))), (uint32_t)ip);
+                const uint32_t tok = x0 & 0xFFu;
                 const int32_t l0 = (int32_t)(tok >> 4), mlc = (int32_t)(tok & 15u);
                 int32_t q = 1, L = l0;
                 bool g = true, sl = false;
@@ -351,7 +333,7 @@ __global__ __launch_bounds__(kPWG) void rows_parse_kernel(const uint8_t* __restr
                     if (ip + 1 >= iend - 15) {
                         g = false;
                     } else {
-                        const int32_t e = (int32_t)((w0.x >> 8) & 0xFFu);
+                        const int32_t e = (int32_t)((x0 >> 8) & 0xFFu);
                         q = 2;
                         L += e;
                         if (ip + 2 > iend - 15) g = false;
@@ -367,7 +349,9 @@ __global__ __launch_bounds__(kPWG) void rows_parse_kernel(const uint8_t* __restr
                     if (po + 3 > 32) {
                         sl = true;
                     } else {
-                        const uint32_t dw = dword32(w0, w1, (uint32_t)(po > 28 ? 28 : po)) >> (8u * (uint32_t)(po > 28 ? po - 28 : 0));
+                        const uint32_t ao = (uint32_t)(ip + po);
+                        const uint32_t dw = __builtin_amdgcn_alignbyte(*(lds_vu32*)(size_t)(Wa | ((ao + 4u) & (kPW - 4))),
+                                                                       *(lds_vu32*)(size_t)(Wa | (ao & (kPW - 4))), ao);
                         const int32_t off = (int32_t)(dw & 0xFFFFu);
                         pq = po + 2;
                         if (mlc == 15) {   // read_variable_length(&ip, iend - 4, 0), one byte of it
@@ -482,39 +466,62 @@ __global__ __launch_bounds__(kPWG) void rows_parse_kernel(const uint8_t* __restr
         }
         // ---- the common sequence, straight-line, until too few lanes can go on
         const int32_t thr = min(kPMinActive, (int)__popcll(__ballot(live)));
-        // two steps per count of the lanes that can go on; every lane runs
-        // both (predicated, no exec-mask branches): a lane that cannot take
-        // its sequence stops (`stall`) -- at its ring's end or a full length
-        // ring until the next general step rotates or flushes, or for a
-        // sequence the fast test does not cover (`need`: the general parse)
-        while (true) {
+        const int32_t kfl = kf + kPStage - 1;   // the length ring is full at k == kfl
+        // the sequence at (ip, op): the token byte, then the aligned dword
+        // pair holding the offset and the match-length byte (each address
+        // wrapped into the ring) -- two dependent LDS reads, no select tree
+        auto peek = [&](int32_t& lit, int32_t& adv, int32_t& ml, int32_t& off, int32_t& oe) __attribute__((always_inline)) {
+            const int32_t tok = (int32_t)*(lds_vu8*)(size_t)(Wa | ((uint32_t)ip & (kPW - 1)));
+            lit = tok >> 4;
+            const int32_t mlc = tok & 15;
+            const int32_t ob = ip + 1 + lit;
+            const uint32_t lo = *(lds_vu32*)(size_t)(Wa | ((uint32_t)ob & (kPW - 4)));
+            const uint32_t hi = *(lds_vu32*)(size_t)(Wa | ((uint32_t)(ob + 4) & (kPW - 4)));
+            const uint32_t dw = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)ob);
+            const bool mlx = mlc == 15;
+            off = (int32_t)(dw & 0xFFFFu);
+            adv = 3 + lit + (int32_t)mlx;
+            ml = mlc + 4 + (mlx ? (int32_t)((dw >> 16) & 0xFFu) : 0);   // 274: a 255 extension byte
+            oe = op + lit + ml;
+        };
+        {
+            // one condition per step for the lanes still going: the ring's
+            // end and the block's end (ip <= iend - 20 covers both end tests
+            // of the reference's fast loop for adv <= 16) as one bound
+            const int32_t lim = min(wb + kPW - 16, iend - 20);
+            const int32_t oendm = oend - 64;
+            // kPSteps steps per count of the lanes still going; every lane runs
+            // them all (predicated, no exec-mask branches), and a lane that
+            // cannot take its sequence stops going
+            bool go = live && !need && !stall;
+            while (true) {
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const bool go = live && !need && !stall;
-                const bool inw = ip + 16 <= wb + kPW;
-                const bool room = k - kf < kPStage - 1;
-                const u32x4 w = ring_ld16(W, ip & (kPW - 1));
-                const int32_t tok = (int32_t)(w.x & 0xFFu), lit = tok >> 4, mlc = tok & 15;
-                const bool mlx = mlc == 15;
-                const uint32_t dw = dword_at(w, (uint32_t)(1 + lit));   // offset, then the match-length byte
-                const int32_t off = (int32_t)(dw & 0xFFFFu);
-                const int32_t ext = (int32_t)((dw >> 16) & 0xFFu);
-                const int32_t adv = 3 + lit + (int32_t)mlx;
-                const int32_t ml = mlc + 4 + (mlx ? ext : 0);
-                const bool fast = (lit <= 12) & !(mlx & (ext == 255)) & (ip + 1 <= iend - 17) &
-                                  (!mlx | (ip + adv <= iend - 4)) & (off != 0) & (off <= op + lit) &
-                                  (op + lit + ml < oend - 64);
-                const bool take = go & inw & room & fast;
-                // slot k is free (one slot of the ring always is): written even
-                // when the sequence is not taken, then overwritten
-                stg[k & (kPStage - 1)] = (uint8_t)adv;
-                ip += take ? adv : 0;
-                op += take ? lit + ml : 0;
-                k += (int32_t)take;
-                stall = stall | (go & !take);
-                need = need | (go & inw & room & !fast);
+                for (int u = 0; u < kPSteps; ++u) {
+                    int32_t lit, adv, ml, off, oe;
+                    peek(lit, adv, ml, off, oe);
+                    const bool take = go & (ip <= lim) & (k < kfl) & (lit <= 12) & (ml != 274) &
+                                      ((uint32_t)(off - 1) < (uint32_t)(op + lit)) & (oe < oendm);
+                    // slot k is free (one slot of the ring always is): written even
+                    // when the sequence is not taken, then overwritten
+                    *(lds_vu8*)(size_t)(Sa | ((uint32_t)k & (kPStage - 1))) = (uint8_t)adv;
+                    ip += take ? adv : 0;
+                    op = take ? oe : op;
+                    k += (int32_t)take;
+                    go = take;
+                }
+                if ((int)__popcll(__ballot(go)) < max(thr, 1)) break;
             }
-            if ((int)__popcll(__ballot(live && !need && !stall)) < max(thr, 1)) break;
+            // a lane that stopped waits (`stall`) for the next general step to
+            // rotate its ring or flush its lengths, or takes the general parse
+            // (`need`) for a sequence the one-step test does not cover
+            if (live && !need && !stall && !go) {
+                int32_t lit, adv, ml, off, oe;
+                peek(lit, adv, ml, off, oe);
+                const bool fast = (lit <= 12) & (ml != 274) & (ip <= iend - 20) & (off != 0) & (off <= op + lit) &
+                                  (oe < oendm);
+                stall = true;
+                need = (ip + 16 <= wb + kPW) & (k < kfl) & !fast;
+            }
         }
     }
 }
@@ -525,11 +532,17 @@ __global__ __launch_bounds__(kPWG) void rows_parse_kernel(const uint8_t* __restr
 // the row knows from the recorded lengths (row prefix sum).  The lengths and
 // the 32 bytes of the NEXT round are requested while this round copies, so a
 // round waits on at most one memory round trip (its far match sources).
-constexpr int32_t kRowsH = 1024;   // history per row (bytes): 1 KiB measured as fast as 2 KiB at equal occupancy
+// History per row (bytes).  Far sources (below the history) are HBM line
+// fills, ~0.67 per sequence at 1 KiB (a 128-byte line for a 16-byte piece):
+// aiming them all at one cached line took the launch 128.6 -> 112.1 ms
+// (r06j, wrong output).  1280 B is the deepest history the LDS holds at 5
+// waves per SIMD (30.8 KB per workgroup; 1392 B ran 4 workgroups per CU,
+// 130.9 ms): 0.61 fills per sequence, 128.6-129.6 -> 127.0-127.3 ms (r06j/k).
+constexpr int32_t kRowsH = 1280;
 constexpr int32_t kRowsHS = kRowsH + 32;   // buffer stride (16-byte reads past the end stay inside)
-constexpr int32_t kRowsKeep = kRowsH / 2;   // history kept on a rebase
-constexpr int32_t kRowsRoom = 512;          // rebase when less room than this is left
-static_assert(kRowsKeep % 16 == 0 && kRowsKeep + kRowsRoom <= kRowsH, "history split");
+constexpr int32_t kRowsRoom = 512;         // rebase when less room than this is left
+constexpr int32_t kRowsKeep = kRowsH - kRowsRoom;   // history kept on a rebase
+static_assert(kRowsKeep % 16 == 0 && kRowsKeep + kRowsRoom <= kRowsH && kRowsKeep + 16 <= 1024, "history split");
 
 // Row-cooperative exact copies in HBM (16 lanes, lane j = jj).
 __device__ __forceinline__ void row_copy_literal(uint8_t* d, const uint8_t* s, int32_t len, int32_t jj) {
@@ -577,7 +590,7 @@ __device__ __forceinline__ void load32(const uint8_t* s, int32_t t, int32_t iend
 // The literal's first 32 bytes go to the lane's LDS slot (two 16-byte
 // aligned entries), not to registers: a parsed round waits there while the
 // previous one executes, and the registers it frees hold the executor at 5
-// waves per SIMD (1 KiB histories).
+// waves per SIMD.
 struct PSeq {
     int32_t t, lit, off, ml, o, dlt;  // t: the literal's input position
     int32_t opn, ipn;                 // uniform across the row
@@ -943,8 +956,8 @@ __global__ __launch_bounds__(kEWG) __attribute__((amdgpu_waves_per_eu(5, 8))) vo
         k0 += (int32_t)(P.fl >> 8);
         const int32_t nbse = next_base(op, base);
         if (nbse != base) {
-            // the kept bytes lie >= kRowsH - kRowsRoom - kRowsKeep past the
-            // buffer start: all reads of a group before its writes
+            // one group (op - nbse < kRowsKeep + 16 <= 1024): every read of
+            // the row's 16 lanes is issued before any write
             for (int32_t c0 = 0; c0 < op - nbse; c0 += 1024) {
                 u32x4 v[4];
 #pragma unroll
