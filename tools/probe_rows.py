@@ -1,6 +1,6 @@
 """Dev probe: decode time per decoder (LZ4M decoders via lz4m_decompress_batch_sel)
 on NBLK x 64 KiB blocks of each KIND, verified against the input.
-env: NBLK (default 262144), KINDS (silesia), DECS (rows,hist), REPS (3)."""
+env: NBLK (default 262144), KINDS (silesia), DECS (rows,hist), REPS (3), SEED (7; the bench: 2026)."""
 import json
 import os
 import sys
@@ -19,7 +19,7 @@ n = int(os.environ.get("NBLK", 262144))
 reps = int(os.environ.get("REPS", 3))
 res = {}
 for kind in os.environ.get("KINDS", "silesia").split(","):
-    src = B.make_batch(n, min(4096, n), kind, 7, dev)
+    src = B.make_batch(n, min(4096, n), kind, int(os.environ.get("SEED", 7)), dev)
     so, sl, slots, soff, scap, olen = B.compress_all(src, n, 0, dev)
     N.launch_compress(src, so, sl, slots, soff, scap, olen, n, N.TABLE_U16_HASH4, 1)
     offs = N.exclusive_scan(olen)
