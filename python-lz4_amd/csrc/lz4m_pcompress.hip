@@ -121,6 +121,17 @@ __device__ __forceinline__ int32_t wave_incl_sum(int32_t v) {
     return v;
 }
 
+// inclusive prefix max across the wave (v >= 0), as wave_incl_sum
+__device__ __forceinline__ int32_t wave_incl_max(int32_t v) {
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false));   // row_shr:1
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false));   // row_shr:2
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false));   // row_shr:4
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false));   // row_shr:8
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false));   // row_bcast:15 -> rows 1, 3
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false));   // row_bcast:31 -> rows 2, 3
+    return v;
+}
+
 // OR of v over the wave (uniform): inclusive prefix OR as wave_incl_sum, read at lane 63
 __device__ __forceinline__ uint32_t wave_or(uint32_t v) {
     v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);   // row_shr:1
@@ -184,16 +195,18 @@ __device__ __forceinline__ int32_t emit_seqs(const uint8_t* s, uint8_t* d, int32
     if (op + total > cap) return -1;
     for (int32_t t0 = 0; t0 < ptotal; t0 += 64) {
         const int32_t t = t0 + (int32_t)lane;
-        // last sequence k < ns with pbase_k <= t (pbase ascends with k)
-        // searched in ds_bpermute byte-address units (4 k): each step's
-        // address is the previous one plus an instruction offset
-        int sq4 = 0;
-#pragma unroll
-        for (int step = 128; step >= 4; step >>= 1) {
-            const int k4 = sq4 + step;
-            const int32_t pk = __builtin_amdgcn_ds_bpermute(k4, pbase);
-            if (k4 < 4 * ns && pk <= t) sq4 = k4;
-        }
+        // last sequence k < ns with pbase_k <= t (pbase ascends with k), in
+        // ds_bpermute byte-address units (4 k): the sequence k0 covering t0 (pbase_0 = 0), then every sequence that
+        // starts inside (t0, t0 + 64) marks its first byte's lane (one forward
+        // permute; lanes with no mark send 0 to lane 0, which k0 covers) and a
+        // prefix max carries the marks up the wave (one LDS round trip where
+        // a 6-step bpermute binary search took six: +0.7-1 %, r06r)
+        const bool sin = (int)lane < ns;
+        const int k0 = (int)__popcll(__ballot(sin && pbase <= t0)) - 1;
+        const int32_t prel = pbase - t0;
+        const bool mk = sin && prel > 0 && prel < 64;
+        const int32_t got = __builtin_amdgcn_ds_permute((mk ? prel : 0) << 2, mk ? (int)lane + 1 : 0);
+        const int sq4 = wave_incl_max(got - 1 > k0 ? got - 1 : k0) << 2;
         const int32_t pb = __builtin_amdgcn_ds_bpermute(sq4, pbase), ob = __builtin_amdgcn_ds_bpermute(sq4, obase),
                       L = __builtin_amdgcn_ds_bpermute(sq4, lit), O = __builtin_amdgcn_ds_bpermute(sq4, off),
                       M = __builtin_amdgcn_ds_bpermute(sq4, ml), S = __builtin_amdgcn_ds_bpermute(sq4, lstart);
