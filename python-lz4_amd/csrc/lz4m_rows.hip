@@ -919,7 +919,7 @@ __global__ __launch_bounds__(kEWG) __attribute__((amdgpu_waves_per_eu(5, 8))) vo
                     u32x4 v = v0;
                     if (!per) {
                         const int32_t sp = s0 + i;
-                        // sp < base: flushed (F >= base + kRowsKeep - 16); the
+                        // sp < base: flushed (F >= base + kRowsKeep - 143); the
                         // second piece of a (not late) far source was requested
                         // with the first; later pieces are loaded now, only where
                         // some lane needs one (this wait then covers only loads
@@ -949,8 +949,15 @@ __global__ __launch_bounds__(kEWG) __attribute__((amdgpu_waves_per_eu(5, 8))) vo
         parse_ahead();
         // ---- flush, advance, rebase for the next round
         const int32_t opn = P.opn;
-        for (int32_t c = F + 16 * jj; c + 16 <= opn; c += 256) st16(d + ROFF(c), lds_ld16(HB + (c - base)));
-        F += (opn - F) & ~15;
+        {
+            // whole 128-byte lines only, each written once (a line split over two
+            // rounds' flushes was written twice: WRITE_SIZE -20 %, the
+            // executor 94.4 -> 90.8 ms, r06x); F lags op by < 144 bytes, all
+            // of them still in the history
+            const int32_t fe = opn & ~127;
+            for (int32_t c = F + 16 * jj; c + 16 <= fe; c += 256) st16(d + ROFF(c), lds_ld16(HB + (c - base)));
+            if (fe > F) F += (fe - F) & ~15;
+        }
         op = opn;
         ip = P.ipn;
         k0 += (int32_t)(P.fl >> 8);
