@@ -487,6 +487,10 @@ __global__ __launch_bounds__(256) void decompress_kernel(const uint8_t* __restri
             if (RESUME) {
                 L.ip = resume[i].ip;
                 L.op = resume[i].op;
+                if (L.ip < 0) {   // a whole-literal block, decoded by rows_parse_kernel: op = its size
+                    L.result = L.op;
+                    L.live = false;
+                }
             }
         }
     }

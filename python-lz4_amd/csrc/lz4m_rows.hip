@@ -189,9 +189,63 @@ __device__ __forceinline__ void load64(const uint8_t* s, int32_t x, int32_t iend
     }
 }
 
+// Whole-literal blocks (an incompressible block: one sequence whose literal
+// runs exactly to the block's end) are decoded here, by the wave: the
+// reference reads the literal length (read_variable_length(&ip, iend - 15, 1),
+// lz4.c:1903-1928: every run byte read leaves ip <= iend - 15), finds
+// ip + length > iend - 32 and takes the last-literals branch (lz4.c:2172-2229),
+// whose result is `length` exactly when ip + length == iend and
+// length <= oend.  The candidate lane f's block is checked here with those
+// tests (anything else is left to the finisher, as before) and its literal
+// copied by the wave, 8 KiB per round trip; the result is the decoded size
+// (-1: not such a block), which the lane records as meta ip = -1 (done), op =
+// the size.  The copy overlaps the other waves' parsing, which is
+// latency-bound; in the finisher it ran at the device's copy rate after the
+// row execution (~2.4 ms of the headline launch's 4 ms finisher).
+__device__ __forceinline__ int64_t whole_literal_block(const uint8_t* s, int32_t iend, int32_t oend, uint8_t* d,
+                                                       uint32_t lane) {
+    typedef __attribute__((address_space(1))) const uint8_t gu8;
+    // the token and the length-byte run: bytes [0, 1024), 16 per lane
+    const int32_t y = 16 * (int32_t)lane;
+    const u32x4 v = y + 16 <= iend ? ld16(s + y) : ld16_guarded(s + y, iend - y);
+    const uint32_t tok = __builtin_amdgcn_readfirstlane(v.x) & 0xFFu;
+    // the first byte other than 255 at position >= 1 in this lane's 16
+    int32_t first = 16;
+    for (int b = 15; b >= 0; --b)
+        if (byte_of(v, b) != 255u && (lane != 0 || b != 0)) first = b;
+    const uint64_t nz = __ballot(first < 16 && y + first < iend);
+    if ((tok >> 4) != 15u || nz == 0) return -1;
+    const int fl = __builtin_ctzll(nz);
+    const int32_t pe = 16 * fl + __builtin_amdgcn_readlane(first, fl);   // the run's last byte
+    const uint32_t bt = (uint32_t)__builtin_amdgcn_readlane((int32_t)byte_of(v, first & 15), fl);
+    const int64_t L = 15 + 255 * (int64_t)(pe - 1) + bt;
+    const int32_t q = pe + 1;
+    if (q > iend - 15 || q + L != (int64_t)iend || L > oend) return -1;
+    // (uniform bases, 32-bit lane offsets: 4 loads in flight per lane)
+    const uint8_t* cs = (const uint8_t*)(gu8*)(s + q);
+    const uint32_t Lf = (uint32_t)L & ~15u;   // whole 16-byte pieces
+    for (uint32_t b = 0; b < Lf; b += 4096) {
+        u32x4 w[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t p = b + 1024u * u + (uint32_t)y;
+            if (p < Lf) w[u] = ld16(cs + p);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t p = b + 1024u * u + (uint32_t)y;
+            if (p < Lf) st16(d + p, w[u]);
+        }
+    }
+    if ((uint32_t)L != Lf && lane == ((Lf >> 4) & 63u)) gbl_put(d + Lf, ld16_guarded(cs + Lf, (int32_t)L - (int32_t)Lf), (int32_t)L - (int32_t)Lf);
+    return L;
+}
+
 __global__ __launch_bounds__(kPWG) void rows_parse_kernel(const uint8_t* __restrict__ src,
                                                          const int64_t* __restrict__ src_off,
                                                          const int32_t* __restrict__ src_len,
+                                                         uint8_t* __restrict__ dst,
+                                                         const int64_t* __restrict__ dst_off,
                                                          const int32_t* __restrict__ dst_cap, int64_t n,
                                                          RowMeta* __restrict__ meta, uint8_t* __restrict__ lens,
                                                          int64_t lens_cap, unsigned long long* __restrict__ ctr) {
@@ -296,6 +350,7 @@ __global__ __launch_bounds__(kPWG) void rows_parse_kernel(const uint8_t* __restr
         // the general parse; every other stopped lane retries the fast loop
         if (live && stall && !need && ip + 16 > wb + kPW) need = true;
         stall = false;
+        bool wl = false;   // a block start with a literal of >= 4 KiB: perhaps a whole-literal block
         if (live && need) {
             need = false;
             if (ip + 32 > wb + kPW) {   // no bytes ahead (block start, a long literal): load the ring now
@@ -393,7 +448,10 @@ __global__ __launch_bounds__(kPWG) void rows_parse_kernel(const uint8_t* __restr
                             // a run past kPRunCap bytes (a literal of >= 4 KiB: an
                             // incompressible block's single literal is ~257) goes to
                             // the finisher: not read byte by byte here, mostly from HBM
-                            if (++run >= kPRunCap && b == 255) good = false;
+                            if (++run >= kPRunCap && b == 255) {
+                                good = false;
+                                wl = k == 0;
+                            }
                         } while (good && b == 255);
                         if (good && (op + lit > oend - 32 || q + lit > iend - 32)) good = false;   // :2016-2027
                     }
@@ -435,6 +493,14 @@ __global__ __launch_bounds__(kPWG) void rows_parse_kernel(const uint8_t* __restr
                 meta[idx] = RowMeta{loff, k, ip, op, 0, 0};
                 live = false;
             }
+        }
+        // whole-literal blocks, checked and copied by the wave (whole_literal_block)
+        for (uint64_t C = __ballot(wl); C != 0; C &= C - 1) {
+            const int f = __builtin_ctzll(C);
+            const int64_t fi = readlane64(idx, f);
+            const int64_t r = whole_literal_block(readlane_ptr(s, f), __builtin_amdgcn_readlane(iend, f),
+                                                  __builtin_amdgcn_readlane(oend, f), dst + dst_off[fi], lane);
+            if ((int)lane == f && r >= 0) meta[idx] = RowMeta{loff, 0, -1, (int32_t)r, 0, 0};
         }
         // flush full halves of the length ring
         if (live && k - kf >= kPStage / 2) {
@@ -554,10 +620,22 @@ __device__ __forceinline__ void row_copy_literal(uint8_t* d, const uint8_t* s, i
 
 __device__ __forceinline__ void row_copy_match(uint8_t* d, int32_t off, int32_t len, int32_t jj) {
     if (off >= 16) {
-        const int32_t w = (off < 256 ? off : 256) & ~15;   // rows whose sources all precede them
+        // steps of w = the offset rounded down to 16 (no piece of a step reads
+        // bytes the step writes), each step's pieces four loads per lane at a
+        // time: a long far match (a zero run's, off ~ ml ~ 2 KB) is one or two
+        // steps, not one fenced 256-byte step each (r06zc)
+        const int32_t w = off & ~15;
         for (int32_t b = 0; b < len; b += w) {
-            const int32_t pos = b + 16 * jj;
-            if (16 * jj < w && pos < len) gbl_put(d + pos, ld16(d + pos - off), len - pos);
+            const int32_t e = min(b + w, len);
+            for (int32_t p0 = b + 16 * jj; p0 < e; p0 += 1024) {
+                u32x4 v[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (p0 + 256 * u < e) v[u] = ld16(d + p0 + 256 * u - off);
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (p0 + 256 * u < e) gbl_put(d + p0 + 256 * u, v[u], len - (p0 + 256 * u));
+            }
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
         }
         return;
@@ -596,7 +674,7 @@ struct PSeq {
     int32_t opn, ipn;                 // uniform across the row
     uint32_t fl;                      // flags | (use << 8): the row takes its first `use` lanes
 };
-constexpr uint32_t kFlU = 1, kFlFar = 2, kFlLate = 4, kFlLitHbm = 8;
+constexpr uint32_t kFlU = 1, kFlFar = 2, kFlLate = 4, kFlLitHbm = 8, kFlEsc = 16;
 
 // The far source's first 32 bytes, requested when the round is parsed (two
 // 16-byte pieces; the second only where a far match is longer than 16 bytes)
@@ -695,7 +773,7 @@ __device__ __forceinline__ void parse_round(PSeq& P, int32_t jj, int32_t r, int3
     P.ml = ml;
     P.o = o;
     P.dlt = dlt;
-    P.fl = ((uint32_t)use << 8) | (u ? kFlU : 0u) | (far ? kFlFar : 0u) | (late ? kFlLate : 0u) |
+    P.fl = ((uint32_t)use << 8) | (u ? kFlU : 0u) | (far ? kFlFar : 0u) | (late ? kFlLate : 0u) | (esc ? kFlEsc : 0u) |
            ((u & (lp + lit > 16) & ((lp + lit > 32) | !wbok)) ? kFlLitHbm : 0u);
 }
 
@@ -818,29 +896,41 @@ __global__ __launch_bounds__(kEWG) __attribute__((amdgpu_waves_per_eu(5, 8))) vo
             // one sequence that does not fit the buffers: flush, copy it in
             // HBM on the row, reload the history
             // (the parse verified it: every read below stays inside the block)
-            const uint32_t tk = s[ip];
-            int32_t L = (int32_t)(tk >> 4), q = ip + 1;
-            if (L == 15) {
-                uint32_t b;
-                do {
-                    b = s[q];
-                    ++q;
-                    L += (int32_t)b;
-                } while (b == 255 && q < iend);
+            int32_t L, q, ofs, qe, M;
+            if (!(row_first((int32_t)P.fl) & kFlEsc)) {   // lane 0's sequence as parse_round read it: exact when not escaped
+                L = row_first(P.lit);
+                q = row_first(P.t);
+                ofs = row_first(P.off);
+                M = row_first(P.ml);
+                // its end: length bytes are runs of 255 and one byte below 255
+                qe = q + L + 2 + (M >= 19 ? (M - 19) / 255 + 1 : 0);
+            } else {   // (rare) a sequence of >= 255 input bytes: byte by byte
+                const uint32_t tk = s[ip];
+                L = (int32_t)(tk >> 4);
+                q = ip + 1;
+                if (L == 15) {
+                    uint32_t b;
+                    do {
+                        b = s[q];
+                        ++q;
+                        L += (int32_t)b;
+                    } while (b == 255 && q < iend);
+                }
+                ofs = (int32_t)s[q + L] | ((int32_t)s[q + L + 1] << 8);
+                qe = q + L + 2;
+                M = (int32_t)(tk & 15u);
+                if (M == 15) {
+                    uint32_t b;
+                    do {
+                        b = s[qe];
+                        ++qe;
+                        M += (int32_t)b;
+                    } while (b == 255 && qe < iend);
+                }
+                M += 4;
             }
-            const int32_t ofs = (int32_t)s[q + L] | ((int32_t)s[q + L + 1] << 8);
-            int32_t qe = q + L + 2, M = (int32_t)(tk & 15u);
-            if (M == 15) {
-                uint32_t b;
-                do {
-                    b = s[qe];
-                    ++qe;
-                    M += (int32_t)b;
-                } while (b == 255 && qe < iend);
-            }
-            M += 4;
+            // the flush and the literal touch different bytes: one fence for both
             for (int32_t c = F + cold_j16(jj); c < op; c += 256) gbl_put(d + c, lds_ld16(HB + (c - base)), op - c);
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
             row_copy_literal(d + op, s + q, L, jj);
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
             row_copy_match(d + op + L, ofs, M, jj);
@@ -1003,7 +1093,7 @@ extern "C" int lz4m_rows_launch(const uint8_t* d_src, const int64_t* d_src_off, 
     hipError_t e = hipMemsetAsync(ctr, 0, 64, stream);
     if (e != hipSuccess) return (int)e;
     hipLaunchKernelGGL(rows_parse_kernel, dim3((uint32_t)parse_grid), dim3(kPWG), 0, stream, d_src, d_src_off,
-                       d_src_len, d_dst_cap, n, meta, lens, lens_cap, ctr);
+                       d_src_len, d_dst, d_dst_off, d_dst_cap, n, meta, lens, lens_cap, ctr);
     hipLaunchKernelGGL(rows_exec_kernel, dim3((uint32_t)exec_grid), dim3(kEWG), 0, stream, d_src, d_src_off, d_src_len,
                        d_dst, d_dst_off, meta, lens, n, ctr);
     return (int)hipGetLastError();

@@ -398,6 +398,60 @@ def test_decompress_kinds_and_sizes(gpu, oracle, kind, block, decoder):
         assert st == len(b) and out == b
 
 
+def _literal_block(payload, tok=0xF0, tail=b""):
+    """One sequence whose literal is `payload` (length bytes as the format
+    writes them), then `tail`: a whole-literal block when tail is empty."""
+    n = len(payload) - 15
+    run = b"\xff" * (n // 255) + bytes([n % 255])
+    return bytes([tok]) + run + payload + tail
+
+
+@pytest.mark.parametrize("decoder", DECODERS)
+def test_decompress_whole_literal_blocks(gpu, oracle, decoder):
+    """Incompressible blocks -- one literal running exactly to the block's end,
+    which the row decoder's parse kernel decodes itself (whole_literal_block,
+    lz4m_rows.hip; the reference's last-literals branch, lz4.c:2172-2229) --
+    and every near miss, which must keep the reference's status: one byte
+    short or long, a capacity one below, a match after the literal, a run
+    longer than the 1 KiB the check reads, a literal shorter than the parse's
+    length-run cap.  Statuses and bytes equal the oracle's."""
+    rng = np.random.default_rng(17)
+    cases, caps = [], []
+    for L in [15, 300, 4094, 4095, 4096, 4110, 4111, 5000, 65535, 65536, 65537, 100_000, 260_000, 270_000]:
+        p = rng.integers(0, 256, size=L, dtype=np.uint8).tobytes()
+        b = _literal_block(p)
+        for cap in (L, L - 1, L + 100, 64):
+            cases.append(b)
+            caps.append(cap)
+        cases += [b[:-1], b + b"x", _literal_block(p, tok=0xFF), _literal_block(p, tail=b"\x05\x00" + b"\x50abcde"),
+                  _literal_block(p, tok=0xF4, tail=b"\x05\x00" + b"\x50abcde")]
+        caps += [L, L + 1, L, L + 13, L + 13]
+    # a length run that never ends inside the block, and one ending on the
+    # read_variable_length limit (ilimit = iend - 15)
+    cases += [b"\xf0" + b"\xff" * 5000, b"\xf0" + b"\xff" * 20 + b"\x01" + b"\x00" * 13]
+    caps += [1 << 20, 1 << 20]
+    # a batch past the row decoder's switch-over for "auto": every 16th block
+    # one of the cases above (up to 64 KiB + 1), the rest 2 KiB pieces of the corpus
+    small = [i for i in range(len(cases)) if len(cases[i]) < 70_000]
+    raw = _synth.blocks(16, "silesia", seed=3).tobytes()
+    pool = [oracle.compress(raw[2048 * i:2048 * (i + 1)]) for i in range(64)]
+    while len(cases) < 33_000:
+        i = len(cases)
+        j = small[(i // 16) % len(small)]
+        cases.append(cases[j] if i % 16 == 0 else pool[i % 64])
+        caps.append(caps[j] if i % 16 == 0 else 2048)
+    res = gpu_decompress(cases, caps, gpu, decoder)
+    memo = {}
+    for i, (s, out) in enumerate(res):
+        key = (cases[i], caps[i])
+        want = memo.get(key)
+        if want is None:
+            want = memo[key] = oracle.decompress(cases[i], caps[i])
+        assert s == want[0], (i, s, want[0], caps[i])
+        if s >= 0:
+            assert out == want[1], i
+
+
 def _offset0_block(lit, ml):
     """A block whose one match has offset 0 (LZ4_decompress_safe v1.9.4 zero-fills
     it) followed by 5 final literals."""
