@@ -868,31 +868,38 @@ __global__ __launch_bounds__(kEWG) __attribute__((amdgpu_waves_per_eu(5, 8))) vo
             have = true;
             sync = true;
         }
+        if (sync && k0 >= nseq) {   // the block's good prefix is done: flush the rest exactly
+            for (int32_t c = F + cold_j16(jj); c < op; c += 256) gbl_put(d + c, lds_ld16(HB + (c - base)), op - c);
+            have = false;
+            continue;
+        }
         if (sync) {   // block start, or the last round stopped early: parse this round now
+            // the length bytes of this round, the next and the one after at
+            // once, then this round's inputs and -- as if it takes all 16 --
+            // the next round's: two round trips before the parse (four were
+            // dependent before, r06ze)
             const int32_t dc = load_len(dl, k0 + jj, nseq);
-            const int32_t tc = ip + row_incl_sum(dc) - dc;
+            const int32_t dq = load_len(dl, k0 + 16 + jj, nseq);
+            lraw = load_len(dl, k0 + 32 + jj, nseq);
+            int32_t incc = dc;
+            incq = dq;
+            row_incl_sum2(incc, incq);
+            const int32_t tc = ip + incc - dc;
             u32x4 wa, wb;
             load_in(s, tc, iend, wa, wb);
+            load_in(s, ip + row_last(incc) + incq - dq, iend, na, nb);   // = P.ipn + incq - dq when P takes 16
             int32_t dummy = 0;
             parse_round(P, jj, r, k0, nseq, ip, op, base, F, s, d, iend, dc, tc, wa, wb, XSL, FS, dummy);
-            const int32_t dq = load_len(dl, k0 + 16 + jj, nseq);
-            incq = row_incl_sum(dq);
-            load_in(s, P.ipn + incq - dq, iend, na, nb);
-            lraw = load_len(dl, k0 + 32 + jj, nseq);
             sync = false;
             // the loads just issued (this round's far sources among them) are
             // waited for here, once: left pending, the merge of this rare path
             // with the common one made every round wait for its newest
-            // far-source request (r05a: -1.7 %)
-            wait_vm0();
+            // far-source request (r05a: -1.7 %).  A round that takes no
+            // sequence goes to the one-sequence path, whose first fence waits.
+            if ((P.fl >> 8) != 0) wait_vm0();
         }
         if ((P.fl >> 8) == 0) {
             sync = true;
-            if (k0 >= nseq) {   // the block's good prefix is done: flush the rest exactly
-                for (int32_t c = F + cold_j16(jj); c < op; c += 256) gbl_put(d + c, lds_ld16(HB + (c - base)), op - c);
-                have = false;
-                continue;
-            }
             // one sequence that does not fit the buffers: flush, copy it in
             // HBM on the row, reload the history
             // (the parse verified it: every read below stays inside the block)
