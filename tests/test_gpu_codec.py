@@ -452,6 +452,56 @@ def test_decompress_whole_literal_blocks(gpu, oracle, decoder):
             assert out == want[1], i
 
 
+def _long_sequence_blocks(n, seed):
+    """Blocks whose sequences do not fit the row decoder's history or its
+    length bytes: literals of 200-700 bytes (compressed length >= 255, the
+    parse's escape), matches of 300-6000 bytes at offsets from 1 to ~5 000
+    (overlapping periodic copies and far ones), zero runs."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(n):
+        b = bytearray()
+        while len(b) < 65536:
+            k = int(rng.integers(0, 5))
+            if k == 0:
+                b += rng.integers(0, 256, size=int(rng.choice([1, 14, 15, 16, 200, 270, 600, 700])), dtype=np.uint8).tobytes()
+            elif k == 1 and len(b) > 16:
+                per = int(rng.choice([1, 2, 3, 7, 15, 16, 17, 40, 300, 900, 1300]))
+                per = min(per, len(b))
+                ml = int(rng.choice([300, 1300, 2000, 6000]))
+                src = bytes(b[-per:])
+                b += (src * (ml // per + 1))[:ml]
+            elif k == 2 and len(b) > 5000:
+                off = int(rng.integers(1300, 5000))
+                ml = int(rng.integers(300, 3000))
+                st = len(b) - off
+                for i in range(ml):
+                    b.append(b[st + i])
+            else:
+                b += bytes(int(rng.integers(64, 4096)))
+        out.append(bytes(b[:65536]))
+    return out
+
+
+@pytest.mark.parametrize("decoder", DECODERS)
+def test_decompress_long_sequences(gpu, oracle, decoder):
+    """Sequences the row decoder takes one at a time (rows_exec_kernel's
+    one-sequence path: the parsed lane-0 values, or a byte-by-byte re-parse of
+    an escaped sequence; far matches in whole-offset steps) and the
+    whole-literal path: bytes and statuses equal the oracle's at the exact
+    capacity and one below."""
+    blocks = _long_sequence_blocks(24, 41)
+    comp = [oracle.compress(b) for b in blocks]
+    cases = comp + comp
+    caps = [65536] * len(comp) + [65535] * len(comp)
+    res = gpu_decompress(cases, caps, gpu, decoder)
+    for i, (s, out) in enumerate(res):
+        want = oracle.decompress(cases[i], caps[i])
+        assert s == want[0], (i, s, want[0])
+        if s >= 0:
+            assert out == want[1], i
+
+
 def _offset0_block(lit, ml):
     """A block whose one match has offset 0 (LZ4_decompress_safe v1.9.4 zero-fills
     it) followed by 5 final literals."""
