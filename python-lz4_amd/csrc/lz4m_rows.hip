@@ -208,7 +208,7 @@ __device__ __forceinline__ int64_t whole_literal_block(const uint8_t* s, int32_t
     // the token and the length-byte run: bytes [0, 1024), 16 per lane
     const int32_t y = 16 * (int32_t)lane;
     const u32x4 v = y + 16 <= iend ? ld16(s + y) : ld16_guarded(s + y, iend - y);
-    const uint32_t tok = __builtin_amdgcn_readfirstlane(v.x) & 0xFFu;
+    const uint32_t tok = (uint32_t)__builtin_amdgcn_readlane((int32_t)v.x, 0) & 0xFFu;   // byte 0: lane 0's
     // the first byte other than 255 at position >= 1 in this lane's 16
     int32_t first = 16;
     for (int b = 15; b >= 0; --b)
