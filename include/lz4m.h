@@ -176,7 +176,8 @@ size_t lz4m_decompress_workspace_bytes(void);
 
 /* Device scratch for the fastest decode of n blocks whose compressed sizes
  * sum to at most src_bytes: 64 + 32 n bytes of counters and per-block
- * records, plus one byte per three compressed bytes for sequence lengths.
+ * records, plus one byte per three compressed bytes for sequence lengths
+ * (each block's lengths start 16-byte aligned: up to 16 more bytes a block).
  * Less scratch is accepted: blocks whose lengths do not fit are decoded by
  * the exact finisher alone, and below 64 + 32 n + 64 bytes the rows decoder
  * is not used. */

@@ -1309,7 +1309,7 @@ extern "C" size_t lz4m_decompress_workspace_bytes(void) { return 64; }
 
 extern "C" size_t lz4m_decompress_workspace_size(int64_t n, int64_t src_bytes) {
     if (n <= 0) return 64;
-    const size_t lens = (size_t)(src_bytes > 0 ? src_bytes : 0) / 3 + 2 * (size_t)n + 64;
+    const size_t lens = (size_t)(src_bytes > 0 ? src_bytes : 0) / 3 + 17 * (size_t)n + 64;   // + 16 per block: 16-aligned lengths
     return (lz4m_rows_fixed_bytes(n) + lens + 255) & ~(size_t)255;
 }
 

@@ -286,9 +286,13 @@ __global__ __launch_bounds__(kPWG) void rows_parse_kernel(const uint8_t* __restr
                         wb = -4 * kPW;
                         pfv = false;
                         if (oend >= 64 && iend > 0) {   // else: no fast loop (lz4.c:1990-1993) or a special case
-                            // a good sequence takes >= 3 input and >= 4 output bytes
+                            // a good sequence takes >= 3 input and >= 4 output bytes;
+                            // rounded up to 16 so that every 16-byte length store is
+                            // aligned inside one 128-byte line (unaligned ones,
+                            // straddling two lines, cost the parse 1.5 ms per 1 M
+                            // blocks, r06zo)
                             const int32_t a = iend / 3, b = oend / 4;
-                            wantb = (int64_t)(a < b ? a : b) + 1;
+                            wantb = ((int64_t)(a < b ? a : b) + 1 + 15) & ~(int64_t)15;
                             fresh = true;
                         } else {
                             meta[idx] = RowMeta{0, 0, 0, 0, 0, 0};
