@@ -258,7 +258,7 @@ __global__ __launch_bounds__(kPWG) void rows_parse_kernel(const uint8_t* __restr
     const uint32_t Sa = (uint32_t)(uintptr_t)stg;   // (kPStage-aligned)
     const uint8_t* s = nullptr;
     int64_t idx = -1, loff = 0;
-    int32_t iend = 0, oend = 0, ip = 0, op = 0, k = 0, kf = 0, wb = 0;
+    int32_t iend = 0, oend = 0, ip = 0, op = 0, k = 0, kf = 0, wb = 0, sh = 0;
     u32x4 pf[4];   // stream bytes [wb + 128, wb + 192), requested ahead
     bool live = false, need = false, more = true, pfv = false, stall = false;
     while (true) {
@@ -279,19 +279,29 @@ __global__ __launch_bounds__(kPWG) void rows_parse_kernel(const uint8_t* __restr
                     const uint64_t below = lane == 0 ? 0 : (idle & (~0ull >> (64 - lane)));
                     idx = (int64_t)(qb + (unsigned long long)__popcll(below));
                     if (idx < n) {
-                        s = src + src_off[idx];
-                        iend = src_len[idx];
+                        // block positions are kept shifted by sh = the block's
+                        // offset in its 64-byte line, so that every ring refill is
+                        // one aligned 64-byte piece (not two partial ones); the
+                        // bytes before the block are read, never parsed -- only
+                        // where they lie inside the caller's buffer
+                        const int64_t so = src_off[idx];
+                        const int32_t il = src_len[idx];
+                        sh = (int32_t)((uintptr_t)(src + so) & 63u);
+                        if (so < sh) sh = 0;
+                        s = src + so - sh;
+                        iend = il + sh;
                         oend = dst_cap[idx];
-                        ip = op = k = kf = 0;
+                        ip = sh;
+                        op = k = kf = 0;
                         wb = -4 * kPW;
                         pfv = false;
-                        if (oend >= 64 && iend > 0) {   // else: no fast loop (lz4.c:1990-1993) or a special case
+                        if (oend >= 64 && il > 0) {   // else: no fast loop (lz4.c:1990-1993) or a special case
                             // a good sequence takes >= 3 input and >= 4 output bytes;
                             // rounded up to 16 so that every 16-byte length store is
                             // aligned inside one 128-byte line (unaligned ones,
                             // straddling two lines, cost the parse 1.5 ms per 1 M
                             // blocks, r06zo)
-                            const int32_t a = iend / 3, b = oend / 4;
+                            const int32_t a = il / 3, b = oend / 4;
                             wantb = ((int64_t)(a < b ? a : b) + 1 + 15) & ~(int64_t)15;
                             fresh = true;
                         } else {
@@ -494,7 +504,7 @@ __global__ __launch_bounds__(kPWG) void rows_parse_kernel(const uint8_t* __restr
                 ++k;
             } else {   // the first sequence that is not good: the finisher resumes here
                 for (int32_t c = kf; c < k; c += 16) gbl_put(lens + loff + c, lds_ld16(stg + (c & (kPStage - 1))), k - c);
-                meta[idx] = RowMeta{loff, k, ip, op, 0, 0};
+                meta[idx] = RowMeta{loff, k, ip - sh, op, 0, 0};
                 live = false;
             }
         }
@@ -502,7 +512,8 @@ __global__ __launch_bounds__(kPWG) void rows_parse_kernel(const uint8_t* __restr
         for (uint64_t C = __ballot(wl); C != 0; C &= C - 1) {
             const int f = __builtin_ctzll(C);
             const int64_t fi = readlane64(idx, f);
-            const int64_t r = whole_literal_block(readlane_ptr(s, f), __builtin_amdgcn_readlane(iend, f),
+            const int32_t fsh = __builtin_amdgcn_readlane(sh, f);
+            const int64_t r = whole_literal_block(readlane_ptr(s, f) + fsh, __builtin_amdgcn_readlane(iend, f) - fsh,
                                                   __builtin_amdgcn_readlane(oend, f), dst + dst_off[fi], lane);
             if ((int)lane == f && r >= 0) meta[idx] = RowMeta{loff, 0, -1, (int32_t)r, 0, 0};
         }

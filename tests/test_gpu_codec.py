@@ -502,6 +502,35 @@ def test_decompress_long_sequences(gpu, oracle, decoder):
             assert out == want[1], i
 
 
+@pytest.mark.parametrize("shift", [1, 13, 63])
+def test_decompress_unaligned_input_base(gpu, oracle, corpus, shift):
+    """The rows parse reads each block through 64-byte windows at absolute
+    line boundaries, starting up to 63 bytes before the block -- but never
+    before the caller's buffer: an input buffer `shift` bytes past a line,
+    first blocks at offsets 0..62 (rows_parse_kernel's `sh`)."""
+    blocks, ragged = corpus
+    src = [b[:17 + 7 * i] for i, b in enumerate(blocks[:9])] + blocks[:24] + ragged
+    comp = [oracle.compress(b) for b in src]
+    packed, offs, lens = _pack(comp)
+    base = torch.zeros(len(packed) + 64 + shift, dtype=torch.uint8, device=gpu)
+    view = base[shift:shift + len(packed)]
+    view.copy_(torch.frombuffer(bytearray(packed), dtype=torch.uint8).to(gpu))
+    caps = [max(len(b), 1) for b in src]
+    d_off = np.concatenate([[0], np.cumsum(caps)[:-1]]).tolist()
+    dst = torch.zeros(sum(caps), dtype=torch.uint8, device=gpu)
+    st = torch.empty(len(src), dtype=torch.int32, device=gpu)
+    N.launch_decompress(view, torch.tensor(offs, dtype=torch.int64, device=gpu),
+                        torch.tensor(lens, dtype=torch.int32, device=gpu), dst,
+                        torch.tensor(d_off, dtype=torch.int64, device=gpu),
+                        torch.tensor(caps, dtype=torch.int32, device=gpu), st, len(src), decoder="rows")
+    host = dst.cpu().numpy()
+    for i, s in enumerate(st.cpu().tolist()):
+        want = oracle.decompress(comp[i], caps[i])
+        assert s == want[0], (i, s, want[0])
+        if s > 0:
+            assert host[d_off[i]:d_off[i] + s].tobytes() == want[1], i
+
+
 def _offset0_block(lit, ml):
     """A block whose one match has offset 0 (LZ4_decompress_safe v1.9.4 zero-fills
     it) followed by 5 final literals."""
